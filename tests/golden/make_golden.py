@@ -1,0 +1,269 @@
+"""Generate the golden label vectors under tests/golden/ from the REFERENCE implementation.
+
+Runs only in the build container (needs /root/reference, read-only).  It imports the
+reference's hot-path modules (picard.config/utils/equations/data/solution) with tiny
+stand-ins for the third-party modules absent from this image (yacs, lightning, h5py,
+tensorboardX, wandb) and with picard/__init__.py bypassed, then injects the
+oracle's Philox noise in the reference's exact draw order:
+
+  1 rand(n,1) t  | 2 [OU] randn(n,nx) x0 | 3 randn_like(x) | 4 randn_like (R,nx) terminal
+  5 rand_like (R,1) s | 6 randn_like (R,nx) integral | 7 [SDGD] randint(0,nx,(R,v))
+
+Terminal/integral normals are the aggregated K-step noise xi_eff = sum_k xi_k / sqrt(K), so
+the reference's one-jump path equals the K-step Euler–Maruyama endpoint.  Outputs (inputs,
+weights, expected labels — data only) are written as .npz fixtures.
+
+Usage:  python tests/golden/make_golden.py
+"""
+import importlib
+import math
+import os
+import shutil
+import sys
+import tempfile
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REF = Path("/root/reference")
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent))
+from oracle import philox as px  # noqa: E402
+
+
+def _install_stubs():
+    class CfgNode(dict):
+        def __init__(self, init=None, new_allowed=False, **kw):
+            super().__init__(init or {})
+
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError as e:
+                raise AttributeError(k) from e
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    yacs = types.ModuleType("yacs")
+    yacs_cfg = types.ModuleType("yacs.config")
+    yacs_cfg.CfgNode = CfgNode
+    yacs.config = yacs_cfg
+    sys.modules["yacs"] = yacs
+    sys.modules["yacs.config"] = yacs_cfg
+
+    class LightningModule(torch.nn.Module):
+        def save_hyperparameters(self, *a, **k):
+            pass
+
+        def log(self, *a, **k):
+            pass
+
+        def log_dict(self, *a, **k):
+            pass
+
+    class _Dummy:
+        def __init__(self, *a, **k):
+            pass
+
+    pl = types.ModuleType("lightning")
+    plp = types.ModuleType("lightning.pytorch")
+    for mod in (pl, plp):
+        mod.LightningModule = LightningModule
+        mod.LightningDataModule = _Dummy
+        mod.Callback = _Dummy
+        mod.Trainer = _Dummy
+    pl.pytorch = plp
+    fab = types.ModuleType("lightning.fabric")
+    fabu = types.ModuleType("lightning.fabric.utilities")
+    fabw = types.ModuleType("lightning.fabric.utilities.warnings")
+    fabw.PossibleUserWarning = UserWarning
+    plu = types.ModuleType("lightning.pytorch.utilities")
+    plut = types.ModuleType("lightning.pytorch.utilities.types")
+    plut.EVAL_DATALOADERS = object
+    for name, mod in {
+        "lightning": pl, "lightning.pytorch": plp, "lightning.fabric": fab,
+        "lightning.fabric.utilities": fabu, "lightning.fabric.utilities.warnings": fabw,
+        "lightning.pytorch.utilities": plu, "lightning.pytorch.utilities.types": plut,
+    }.items():
+        sys.modules[name] = mod
+    h5 = types.ModuleType("h5py")
+    h5.File = _Dummy
+    sys.modules["h5py"] = h5
+    tbx = types.ModuleType("tensorboardX")
+    tbx.SummaryWriter = _Dummy
+    sys.modules["tensorboardX"] = tbx
+    pkg = types.ModuleType("picard")
+    pkg.__path__ = [str(REF / "picard")]
+    sys.modules["picard"] = pkg
+    return CfgNode
+
+
+CfgNode = _install_stubs()
+eqs = importlib.import_module("picard.equations")
+data = importlib.import_module("picard.data")
+sols = importlib.import_module("picard.solution")
+
+
+class NoiseQueue:
+    """Replace torch's RNG entry points with pops from a queue (shape-checked)."""
+
+    def __init__(self, items):
+        self.items = list(items)
+        self.orig = {}
+
+    def _pop(self, kind, shape):
+        k, arr = self.items.pop(0)
+        assert k == kind, f"draw order mismatch: expected {k}, reference asked for {kind}"
+        assert tuple(arr.shape) == tuple(shape), f"{kind}: shape {arr.shape} vs {shape}"
+        return torch.as_tensor(arr)
+
+    def __enter__(self):
+        self.orig = {n: getattr(torch, n) for n in ("rand", "randn", "randn_like", "rand_like", "randint")}
+        q = self
+
+        def rand(*size, **kw):
+            size = size[0] if len(size) == 1 and isinstance(size[0], (tuple, list)) else size
+            return q._pop("rand", size).to(torch.get_default_dtype())
+
+        def randn(*size, **kw):
+            size = size[0] if len(size) == 1 and isinstance(size[0], (tuple, list)) else size
+            return q._pop("randn", size).to(torch.get_default_dtype())
+
+        def randn_like(x, **kw):
+            return q._pop("randn", x.shape).to(x.dtype)
+
+        def rand_like(x, **kw):
+            return q._pop("rand", x.shape).to(x.dtype)
+
+        def randint(low, high, size, **kw):
+            return q._pop("randint", size).to(torch.int64)
+
+        torch.rand, torch.randn, torch.randn_like, torch.rand_like, torch.randint = (
+            rand, randn, randn_like, rand_like, randint)
+        return self
+
+    def __exit__(self, *a):
+        for n, f in self.orig.items():
+            setattr(torch, n, f)
+        assert not self.items, f"{len(self.items)} injected draws unused"
+
+
+def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v):
+    i = point_base + np.arange(n)
+    items = [("rand", px.uniforms(px.TAG_T, epoch, seed, i, 0)[:, None])]
+    if eq_name == "OUProcessEquation":
+        items.append(("randn", px.normals(px.TAG_X0, epoch, seed, i, 0, 0, nx)))
+    items.append(("randn", px.normals(px.TAG_X, epoch, seed, i, 0, 0, nx)))
+    ii = i[:, None]
+    mm = np.arange(M)[None, :]
+    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, mm, k, nx) for k in range(K))
+    S_s = sum(px.normals(px.TAG_INT, epoch, seed, ii, mm, k, nx) for k in range(K))
+    items.append(("randn", (S_T / math.sqrt(K)).reshape(n * M, nx)))
+    items.append(("rand", px.uniforms(px.TAG_S, epoch, seed, ii, mm, open_low=True).reshape(n * M, 1)))
+    items.append(("randn", (S_s / math.sqrt(K)).reshape(n * M, nx)))
+    if v > 0:
+        items.append(("randint", px.randint_idx(px.TAG_SDGD, epoch, seed, ii, mm, v, nx).reshape(n * M, v)))
+    return items
+
+
+def make_equation(name, kw, workdir):
+    cwd = os.getcwd()
+    os.chdir(workdir)
+    try:
+        return getattr(eqs, name)(**kw)
+    finally:
+        os.chdir(cwd)
+
+
+def prepare_workdir():
+    wd = Path(tempfile.mkdtemp(prefix="dpi_golden_"))
+    for f in (REF / "scripts/fully_nonlinear/case_1").glob("*.pt"):
+        shutil.copy(f, wd / f.name)
+    for f in (REF / "scripts/hjb").glob("*.pt"):
+        shutil.copy(f, wd / f.name)
+    # finding 8: var file is not shipped; it is deterministic var_scale * I
+    torch.save(torch.stack([2.0 * torch.eye(100, dtype=torch.float64) for _ in range(5)]),
+               wd / "var_100d_ms=1.0_vs=2.0_5.pt")
+    return wd
+
+
+def state_dict_np(module):
+    return {k: v.detach().cpu().numpy() for k, v in module.state_dict().items()}
+
+
+def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, point_base=0, v=0,
+             init_seed=0, workdir=None, zero=False, weight_scale=1.0):
+    torch.set_default_dtype(torch.float64)
+    eq = make_equation(eq_name, eq_kw, workdir)
+    torch.manual_seed(init_seed)
+    if zero:
+        net = sols.ZeroSolution(1)
+    elif net_kind == "mlp":
+        net = sols.construct_mlp(1 + eq.nx, 1, net_kw["neurons"], ["ELU"] * len(net_kw["neurons"]), None)
+    else:
+        net = sols.PISGradNet(hidden_shapes=net_kw["neurons"], dim=eq.nx, g0=eq.g, T=eq.T)
+    if weight_scale != 1.0:
+        with torch.no_grad():
+            for p in net.parameters():
+                p.mul_(weight_scale)
+    if net_kind == "pis" and not zero:
+        with torch.no_grad():  # a non-trivial learnable phase
+            net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
+    hess = CfgNode({"method": "SDGD" if v > 0 else None, "kwargs": CfgNode({"v": v} if v > 0 else {})})
+    gen = data.OnlineDataGenerator(
+        eq, net, 1, 1, device="cpu", t_always_uniform=True, n_estimate_terminal=M,
+        n_estimate_integral=M, hessian_approximation=hess, sample_bound=None,
+        estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=0.0)
+    items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v)
+    with NoiseQueue(items):
+        tx, y = gen.sample_with_gradients(n)
+    out = {
+        "case": name, "eq": eq_name, "net": "zero" if zero else net_kind, "n": n, "M": M, "K": K,
+        "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v,
+        "tx": tx.numpy(), "y": y.detach().numpy(),
+    }
+    for k, val in eq_kw.items():
+        out[f"eqkw_{k}"] = val
+    if not zero:
+        for k, val in state_dict_np(net).items():
+            out[f"sd_{k}"] = val
+        out["neurons"] = np.asarray(net_kw["neurons"])
+    if eq_name == "OUProcessEquation":
+        out["gmm_mean"] = eq.mean.numpy()
+        out["gmm_var"] = torch.diagonal(eq.var, dim1=1, dim2=2).numpy()
+        out["gmm_pi"] = eq.pi.numpy()
+    if eq_name == "GBMEquationComplexExact":
+        out["gbm_w"] = eq.w.numpy()
+        out["gbm_v"] = eq.v.numpy()
+    np.savez_compressed(HERE / f"{name}.npz", **out)
+    print(f"{name}: tx {tx.shape} y {y.shape} |y|={float(y.norm()):.4g}")
+
+
+def main():
+    wd = prepare_workdir()
+    cha = {"nx": 100, "alpha": 1.0, "k": 5.0, "T": 1.0}
+    ou = {"nx": 100, "alpha": 1.0, "T": 1.0, "num_components": 5, "mean_scale": 1.0,
+          "var_scale": 2.0, "alpha_scale": 4.0}
+    gbm = {"nx": 100, "alpha": 1.0, "T": 1.0}
+    # Burgers: small MLP, several K; full-width 4x128 (config 1 network) at K=20; zero net
+    run_case("cha_mlp16_K1", "Cha", cha, "mlp", {"neurons": [16, 16]}, 4, 64, 1, 20250725, workdir=wd)
+    run_case("cha_mlp16_K4", "Cha", cha, "mlp", {"neurons": [16, 16]}, 4, 64, 4, 7, epoch=3, point_base=100, workdir=wd)
+    run_case("cha_mlp128x4_K20", "Cha", cha, "mlp", {"neurons": [128] * 4}, 3, 64, 20, 20250725, workdir=wd)
+    run_case("cha_zero_K2", "Cha", cha, "mlp", {"neurons": [8]}, 3, 32, 2, 11, workdir=wd, zero=True)
+    # HJB: OU + GMM, PISGradNet (reduced width), zero net (iteration 1)
+    run_case("ou_pis32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 3, 32, 2, 2, workdir=wd)
+    run_case("ou_mlp16_K2", "OUProcessEquation", ou, "mlp", {"neurons": [16, 16]}, 3, 32, 2, 5, workdir=wd)
+    run_case("ou_zero_K1", "OUProcessEquation", ou, "mlp", {"neurons": [8]}, 3, 32, 1, 2, workdir=wd, zero=True)
+    # Fully-nonlinear case_1 (GBM): SDGD v=100 and full-Hessian (v=0), MLP 3x16
+    run_case("gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 3, 32, 2, 3,
+             v=100, workdir=wd)
+    run_case("gbm_mlp16_full_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 16, 1, 4,
+             workdir=wd)
+    shutil.rmtree(wd)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,45 @@
+"""Helpers: load golden fixtures (tests/golden/*.npz) into oracle objects."""
+from pathlib import Path
+
+import numpy as np
+
+from oracle import dpi_oracle as O
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+CASES = sorted(p.stem for p in GOLDEN.glob("*.npz"))
+
+
+def load(name):
+    z = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+    return {k: z[k] for k in z.files}
+
+
+def oracle_equation(f):
+    eq = str(f["eq"])
+    if eq == "Cha":
+        return O.Cha(int(f["eqkw_nx"]), float(f["eqkw_alpha"]), float(f["eqkw_k"]), float(f["eqkw_T"]))
+    if eq == "OUProcessEquation":
+        return O.OUProcessEquation(int(f["eqkw_nx"]), f["gmm_mean"], f["gmm_var"], f["gmm_pi"],
+                                   alpha=float(f["eqkw_alpha"]), T=float(f["eqkw_T"]),
+                                   alpha_scale=float(f["eqkw_alpha_scale"]))
+    if eq == "GBMEquationComplexExact":
+        return O.GBMEquationComplexExact(int(f["eqkw_nx"]), f["gbm_w"], f["gbm_v"],
+                                         alpha=float(f["eqkw_alpha"]), T=float(f["eqkw_T"]))
+    raise ValueError(eq)
+
+
+def state_dict(f):
+    return {k[3:]: f[k] for k in f if k.startswith("sd_")}
+
+
+def oracle_net(f, eq):
+    kind = str(f["net"])
+    if kind == "zero":
+        return O.ZeroNet()
+    sd = state_dict(f)
+    if kind == "mlp":
+        idx = sorted({int(k.split(".")[0]) for k in sd})
+        Ws = [sd[f"{i}.weight"] for i in idx]
+        bs = [sd[f"{i}.bias"] for i in idx]
+        return O.MLP(Ws, bs, ["ELU"] * (len(Ws) - 1))
+    return O.PISGradNet(sd, eq, T=eq.T)
