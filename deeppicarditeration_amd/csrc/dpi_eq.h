@@ -1,0 +1,93 @@
+// Equation plugins as device functors (picard/equations.py problem API, compiled).
+//
+// The terminal payoff g and the nonlinearity f of every shipped equation are written as
+//   g(X) = G(sum_d phi_c(d, X_d))  (a few separable per-path statistics + a scalar finish),
+//   f(s, X, u, grad u) from u, sum_d grad_d u, sum_d (X_d - mu) grad_d u, sum_d (grad_d u)^2,
+// so a path's dims can be spread over lanes/waves and combined by fixed-order reductions.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/dpi.h"
+
+namespace dpi {
+
+constexpr int NSG = 8;  // max per-path g statistics (OU mixture components)
+
+struct EqDev {
+  int kind, nx;
+  float T, alpha, asq;  // asq = sqrt(alpha)
+  // Cha (equations.py:266-338): k' = k / sqrt(nx); ff(w) = alpha (k' y - C) sum w
+  float cha_k, cha_C;
+  // OUProcessEquation (equations.py:599-714)
+  float ou_theta, ou_mu, ou_d;
+  int ncomp;
+  const float* mean;  // (ncomp, nx)
+  const float* ivar;  // (ncomp, nx) 1/var
+  const float* logc;  // (ncomp) log pi_k - 0.5 (nx log 2pi + log det_k)   (utils.py:862-876)
+  // GBMEquationComplexExact (equations.py:388-486)
+  int nodes;
+  const float* gw;  // (nodes, 1+nx)
+  const float* gv;  // (nodes)
+};
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+template <int KIND>
+struct Eq;
+
+// ------------------------------------------------------------------------------ Cha
+template <>
+struct Eq<DPI_EQ_CHA> {
+  static constexpr int GRAD_FULL = 0;  // fff only needs sum_d z_d (equations.py:297-302)
+  __device__ static __forceinline__ void gstat(const EqDev& e, int d, float X, float* st) { st[0] += X; }
+  __device__ static __forceinline__ float gfin(const EqDev& e, const float* st) {
+    return sigmoidf_(e.T + e.cha_k * st[0]);  // equations.py:304-305
+  }
+  __device__ static __forceinline__ void gacc(const EqDev& e, int d, float X, float z, float& A, float& B) {}
+  // f = ffv + ffc: the state-independent constant is kept apart so f - f_b never cancels it in fp32
+  __device__ static __forceinline__ float ffv(const EqDev& e, float u, float gsum, float A, float B) {
+    return e.alpha * (e.cha_k * u - e.cha_C) * gsum;  // ff(w) = fff(sqrt(alpha) w), :199-200
+  }
+  __device__ static __forceinline__ float ffc(const EqDev& e) { return 0.f; }
+};
+
+// ------------------------------------------------------------------------------ OU (HJB)
+template <>
+struct Eq<DPI_EQ_OU> {
+  static constexpr int GRAD_FULL = 1;
+  __device__ static __forceinline__ void gstat(const EqDev& e, int d, float X, float* st) {
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      if (c < e.ncomp) {
+        const float df = X - e.mean[c * e.nx + d];
+        st[c] = fmaf(df * df, e.ivar[c * e.nx + d], st[c]);
+      }
+    }
+  }
+  __device__ static __forceinline__ float gfin(const EqDev& e, const float* st) {
+    // g = -log sum_k exp(logc_k - 0.5 st_k)    (equations.py:592-593, utils.py:852-880)
+    float lp[NSG];
+    float mx = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      lp[c] = (c < e.ncomp) ? e.logc[c] - 0.5f * st[c] : -3.0e38f;
+      mx = fmaxf(mx, lp[c]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      if (c < e.ncomp) s += __expf(lp[c] - mx);
+    return -(mx + __logf(s));
+  }
+  __device__ static __forceinline__ void gacc(const EqDev& e, int d, float X, float z, float& A, float& B) {
+    A = fmaf(X - e.ou_mu, z, A);
+    B = fmaf(z, z, B);
+  }
+  // -(theta (mu - x)) . z - alpha/2 |z|^2 - d theta    (equations.py:660-666) = ffv + ffc
+  __device__ static __forceinline__ float ffv(const EqDev& e, float u, float gsum, float A, float B) {
+    return e.ou_theta * A - 0.5f * e.alpha * B;
+  }
+  __device__ static __forceinline__ float ffc(const EqDev& e) { return -e.ou_d * e.ou_theta; }
+};
+
+}  // namespace dpi

@@ -1,0 +1,1067 @@
+// MI355X (gfx950) kernels of the DPI label-generation hot path + the C-ABI of include/dpi.h.
+//
+// One workgroup (256 threads = 4 waves) owns one collocation point i and 64 consecutive
+// Monte-Carlo indices m.  Per workgroup:
+//   phase 1  (VALU)  Philox4x32-10 + Box–Muller noise, K-step Euler–Maruyama rollout of the
+//                    terminal path (t -> T) and the integral path (t -> s), 100 dims each.
+//                    Lane = path; a wave owns whole 4-dim blocks, so Philox counters other
+//                    than m are wave-uniform.  Terminal sums stay in registers, integral
+//                    sums go to LDS as the MFMA B operand; g(X_T) statistics are reduced
+//                    over waves in fixed order.
+//   phase 2  (MFMA)  u(s, X_s) and its input gradient for the 64 paths: the MLP as
+//                    v_mfma_f32_16x16x4_f32 tiles, hidden x paths orientation (wave = 16
+//                    paths), activations kept in registers as the next layer's B operand,
+//                    weights staged through LDS 32 rows at a time, backward via the
+//                    transposed weights.  X_s = x + c_p S is never formed: layer 1 is
+//                    z = (W1x x + b1) + W1t s + c_p (W1x S).
+//   phase 3          per-path contributions (g(X_T)-g(x))(1,Y_T) + (T-t)(f-f_b)(1,Y_s)
+//                    reduced over the 64 lanes into a per-(point, block) partial slab.
+// A pairwise reduce kernel then sums the blocks in a fixed tree (bit-reproducible; equal
+// for any split of the blocks over GPUs aligned to powers of two) and a finalize kernel
+// divides by M, adds g(x) and clips (picard/data.py:924-926, :525-526, :222).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dpi.h"
+#include "dpi_eq.h"
+#include "dpi_rng.h"
+
+namespace dpi {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int P = DPI_PATH_BLOCK;  // 64 paths per workgroup
+constexpr int NTH = 256;           // threads per workgroup
+constexpr int SS = P + 4;          // LDS row stride of the [dim][path] noise tile (bank-conflict free)
+constexpr int WST = 136;           // LDS row stride of a staged weight chunk (WST/4 = 2 mod 4)
+constexpr int NXP_MAX = 128;       // max padded state dimension
+constexpr int HMAX = 128;
+
+struct NetDev {
+  int kind;  // 0 zero, 1 mlp
+  int H, L, nxp;
+  const float* W1x;   // (H, nxp)   W1[:, 1:]
+  const float* w1t;   // (H)        W1[:, 0]
+  const float* b1;    // (H)
+  const float* c1;    // (H)        sum_d W1[h, 1+d]
+  const float* W1xT;  // (nxp, H)
+  const float* W[4];  // (H, H) hidden layer l = 1..L-1
+  const float* WT[4];
+  const float* b[4];
+  const float* wout;  // (H)
+  float bout;
+};
+
+// ------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float elu(float z) { return z > 0.f ? z : __expf(z) - 1.0f; }
+__device__ __forceinline__ float delu_from_a(float a) { return a > 0.f ? 1.0f : a + 1.0f; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// sum over the 4 lane groups (lanes j, j+16, j+32, j+48) of the MFMA C layout
+__device__ __forceinline__ float qsum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// Stage rows [r0, r0 + nrows) of a row-major global matrix with ncol floats per row
+// (ncol % 4 == 0) into LDS rows of stride WST.
+__device__ __forceinline__ void stage_rows(const float* __restrict__ g, int ncol, int r0, int nrows, float* wsh) {
+  const int nf4 = ncol >> 2;
+  for (int idx = threadIdx.x; idx < nrows * nf4; idx += NTH) {
+    const int r = idx / nf4, c = idx - r * nf4;
+    const float4 v = *reinterpret_cast<const float4*>(g + (size_t)(r0 + r) * ncol + 4 * c);
+    *reinterpret_cast<float4*>(wsh + r * WST + 4 * c) = v;
+  }
+}
+
+// LDS layout (floats) shared by the baseline and path kernels.
+struct Lds {
+  float S[NXP_MAX * SS];   // [dim][path] integral noise sums (path kernel) / x tile (baseline)
+  float W[32 * WST];       // weight chunk
+  float vec[6 * HMAX];     // base0 | w1t | b1(layer bias l) ... | wout | c1
+  float bh[4 * HMAX];      // hidden-layer biases
+  float xsh[NXP_MAX];      // point x (path kernel) / zeros (baseline)
+  float gst[4 * P * NSG];  // per-wave partial g statistics
+  float tau[P], cmul[P], bsh[P];
+};
+
+// ------------------------------------------------------------------------------ MLP tile
+// u and gradient terms for the 16 paths of this wave (path column pp = 16*wave + (lane&15)).
+// Inputs (all in LDS): S tile [d][p], xsh (X_d = xsh[d] + cmul_p * S[d][p]), tau (time input),
+// cmul, vec[0:H] = base0 (layer-1 bias incl. W1x x), vec[H:2H] = w1t, vec[2H:3H] = wout,
+// vec[3H:4H] = c1, bh[l*H:(l+1)*H] = biases of hidden layers l >= 1.
+// If bx_out != nullptr (baseline mode) writes b1 + W1x S (per path) to bx_out[pp*bstride + h].
+template <int KIND, int H, int L>
+__device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, Lds& sh, int nxt, float& u_out,
+                                         float& gsum_out, float& gA_out, float& gB_out, float* bx_out,
+                                         int bstride, int n_valid_paths) {
+  constexpr int HT = H / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  float act[L][HT][4];
+
+  // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+#pragma unroll
+  for (int T0 = 0; T0 < HT; T0 += 2) {
+    const int nr = (HT - T0) >= 2 ? 32 : 16;
+    __syncthreads();
+    stage_rows(net.W1x, net.nxp, 16 * T0, nr, sh.W);
+    __syncthreads();
+#pragma unroll
+    for (int T2 = 0; T2 < 2; ++T2) {
+      const int T = T0 + T2;
+      if (T < HT) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+        for (int t = 0; t < nxt; ++t) {
+          const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+          const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+          acc = mfma4(a.x, bc[0], acc);
+          acc = mfma4(a.y, bc[SS], acc);
+          acc = mfma4(a.z, bc[2 * SS], acc);
+          acc = mfma4(a.w, bc[3 * SS], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * T + 4 * qq + r;
+          const float z = fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h]));
+          act[0][T][r] = elu(z);
+          if (bx_out && pp < n_valid_paths) bx_out[(size_t)pp * bstride + h] = sh.vec[h] + acc[r];
+        }
+      }
+    }
+  }
+  // ---------------- hidden layers
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      const int nr = (HT - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.W[l], H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < HT) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[l - 1][t][0], acc);
+            acc = mfma4(a.y, act[l - 1][t][1], acc);
+            acc = mfma4(a.z, act[l - 1][t][2], acc);
+            acc = mfma4(a.w, act[l - 1][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = 16 * T + 4 * qq + r;
+            act[l][T][r] = elu(acc[r] + sh.bh[l * H + h]);
+          }
+        }
+      }
+    }
+  }
+  // ---------------- output u = wout . a_L + bout ; delta_L = wout * elu'(a_L)
+  float up = 0.f;
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      const float w = sh.vec[2 * H + h];
+      up = fmaf(w, act[L - 1][T][r], up);
+      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+    }
+  u_out = qsum(up) + net.bout;
+  // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      const int nr = (HT - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.WT[l + 1], H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < HT) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[l + 1][t][0], acc);
+            acc = mfma4(a.y, act[l + 1][t][1], acc);
+            acc = mfma4(a.z, act[l + 1][t][2], acc);
+            acc = mfma4(a.w, act[l + 1][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) act[l][T][r] = acc[r] * delu_from_a(act[l][T][r]);
+        }
+      }
+    }
+  }
+  // ---------------- input gradient
+  if (!Eq<KIND>::GRAD_FULL) {
+    float gp = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp = fmaf(sh.vec[3 * H + 16 * T + 4 * qq + r], act[0][T][r], gp);
+    gsum_out = qsum(gp);
+    gA_out = gB_out = 0.f;
+  } else {
+    float A = 0.f, B = 0.f;
+    for (int T0 = 0; T0 < nxt; T0 += 2) {
+      const int nr = (nxt - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.W1xT, H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < nxt) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[0][t][0], acc);
+            acc = mfma4(a.y, act[0][t][1], acc);
+            acc = mfma4(a.z, act[0][t][2], acc);
+            acc = mfma4(a.w, act[0][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = 16 * T + 4 * qq + r;
+            if (d < e.nx) {
+              const float X = fmaf(cm, sh.S[d * SS + pp], sh.xsh[d]);
+              Eq<KIND>::gacc(e, d, X, acc[r], A, B);
+            }
+          }
+        }
+      }
+    }
+    gA_out = qsum(A);
+    gB_out = qsum(B);
+    gsum_out = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------------ kernels
+// Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
+template <int KIND>
+__global__ void k_sample_points(EqDev e, int n, uint32_t k0, uint32_t k1, uint32_t c3t, uint32_t c3x0,
+                                uint32_t c3x, uint32_t point_base, float eps, float alpha_init_sqrt, float* tx) {
+  const int nb = (e.nx + 3) >> 2;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = gid / nb, j = gid - i * nb;
+  if (i >= n) return;
+  const uint32_t ig = point_base + (uint32_t)i;
+  const float U = u01_co(philox4x32_10(0u, 0u, ig, c3t, k0, k1).x);
+  const float t = (e.T - 2.f * eps) * (1.f - U) + eps;
+  float* row = tx + (size_t)i * (1 + e.nx);
+  if (j == 0) row[0] = t;
+  const f4 z = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x, k0, k1));
+  f4 z0 = {0.f, 0.f, 0.f, 0.f};
+  if (KIND == DPI_EQ_OU) {
+    z0 = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x0, k0, k1));
+    z0.a *= alpha_init_sqrt;
+    z0.b *= alpha_init_sqrt;
+    z0.c *= alpha_init_sqrt;
+    z0.d *= alpha_init_sqrt;
+  }
+  const float sc = sqrtf(t) * e.asq;
+  const float zz[4] = {z.a, z.b, z.c, z.d};
+  const float xx[4] = {z0.a, z0.b, z0.c, z0.d};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int d = 4 * j + q;
+    if (d < e.nx) row[1 + d] = fmaf(sc, zz[q], xx[q]);
+  }
+}
+
+// Block-wide sum over 256 threads (result on every thread); red: >= 4 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// Baseline per point (one workgroup per point): g(x), the state-dependent part of
+// f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
+// f_baseline).  A latency-bound handful of points, so one thread per hidden unit computes its
+// fp32 dot product (weights read coalesced through the transposed copies), no LDS staging.
+template <int KIND, bool ZERO>
+__global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
+                                                  float* __restrict__ gx, float* __restrict__ fb,
+                                                  float* __restrict__ bx) {
+  __shared__ float xs[NXP_MAX];
+  __shared__ float act[4][HMAX];
+  __shared__ float dbuf[2][HMAX];
+  __shared__ float red[8];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int nx = e.nx, F = 1 + nx;
+  const float* row = tx + (size_t)i * F;
+  const float t = row[0];
+  for (int d = tid; d < NXP_MAX; d += NTH) xs[d] = d < nx ? row[1 + d] : 0.f;
+  __syncthreads();
+  // g(x): per-thread dims, then per-statistic block sums in fixed order
+  {
+    float st[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = 0.f;
+    for (int d = tid; d < nx; d += NTH) Eq<KIND>::gstat(e, d, xs[d], st);
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = block_sum(st[c], red);
+    if (tid == 0) gx[i] = Eq<KIND>::gfin(e, st);
+  }
+  if (ZERO) {
+    if (tid == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int H = net.H, L = net.L, nxp = net.nxp;
+  // layer 1
+  if (tid < H) {
+    float acc = 0.f;
+    for (int d = 0; d < nx; ++d) acc = fmaf(net.W1xT[(size_t)d * H + tid], xs[d], acc);
+    bx[(size_t)i * H + tid] = net.b1[tid] + acc;
+    act[0][tid] = elu(fmaf(net.w1t[tid], t, net.b1[tid] + acc));
+  }
+  __syncthreads();
+  for (int l = 1; l < L; ++l) {
+    if (tid < H) {
+      float acc = net.b[l][tid];
+      const float* wt = net.WT[l];
+      for (int k = 0; k < H; ++k) acc = fmaf(wt[(size_t)k * H + tid], act[l - 1][k], acc);
+      act[l][tid] = elu(acc);
+    }
+    __syncthreads();
+  }
+  const float u = block_sum(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
+  int cur = 0;
+  if (tid < H) dbuf[0][tid] = net.wout[tid] * delu_from_a(act[L - 1][tid]);
+  __syncthreads();
+  for (int l = L - 2; l >= 0; --l) {
+    if (tid < H) {
+      const float* w = net.W[l + 1];  // (H_out, H_in) row-major: column tid is coalesced across threads
+      float acc = 0.f;
+      for (int k = 0; k < H; ++k) acc = fmaf(w[(size_t)k * H + tid], dbuf[cur][k], acc);
+      dbuf[cur ^ 1][tid] = acc * delu_from_a(act[l][tid]);
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  float gs = 0.f, gA = 0.f, gB = 0.f;
+  if (!Eq<KIND>::GRAD_FULL) {
+    gs = block_sum(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
+  } else {
+    float A = 0.f, B = 0.f;
+    for (int d = tid; d < nx; d += NTH) {
+      float z = 0.f;
+      for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], dbuf[cur][k], z);
+      Eq<KIND>::gacc(e, d, xs[d], z, A, B);
+    }
+    gA = block_sum(A, red);
+    gB = block_sum(B, red);
+  }
+  if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
+}
+
+struct PathArgs {
+  const float* tx;
+  const float* gx;
+  const float* fb;
+  const float* bx;
+  float* partial;
+  int n, nbp, m_begin, K, flags;
+  uint32_t k0, k1, c3t, c3s, c3i, point_base;
+};
+
+// One workgroup = (point i, 64 consecutive MC indices).  See the file header.
+template <int KIND, int H, int L, bool ZERO>
+__global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+  __shared__ Lds sh;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = blockIdx.x / a.nbp, blk = blockIdx.x - i * a.nbp;
+  const uint32_t ig = a.point_base + (uint32_t)i;
+  const uint32_t m = (uint32_t)(a.m_begin + P * blk + lane);
+  const int nx = e.nx, F = 1 + nx;
+  const int nb = (nx + 3) >> 2;
+  const int nxp = ZERO ? ((nx + 15) & ~15) : net.nxp;
+  const bool TERM = a.flags & DPI_TERMINAL, INTG = a.flags & DPI_INTEGRAL;
+  const float* txr = a.tx + (size_t)i * F;
+  const float t = txr[0];
+  const float tmt = e.T - t;
+  const float g_x = a.gx[i], f_b = a.fb[i];
+  const float Kf = (float)a.K;
+
+  for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
+  for (int idx = tid; idx < (nxp - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
+    const int d = 4 * nb + idx / P, p = idx % P;
+    sh.S[d * SS + p] = 0.f;
+  }
+  if (!ZERO) {
+    for (int h = tid; h < H; h += NTH) {
+      sh.vec[h] = a.bx[(size_t)i * H + h];  // b1 + W1x x (from k_baseline)
+      sh.vec[H + h] = net.w1t[h];
+      sh.vec[2 * H + h] = net.wout[h];
+      sh.vec[3 * H + h] = net.c1[h];
+    }
+    for (int l = 1; l < L; ++l)
+      for (int h = tid; h < H; h += NTH) sh.bh[l * H + h] = net.b[l][h];
+  }
+  // s ~ U(t, T] for this lane's path (data.py:359); integral/terminal step multipliers
+  const float U = u01_oc(philox4x32_10(0u, m, ig, a.c3s, a.k0, a.k1).x);
+  const float s = fmaf(U, tmt, t);
+  const float smt = s - t;
+  const float cI = e.asq * sqrtf(smt / Kf);            // X_s = x + cI * sum_k xi_k
+  const float yI = 1.0f / (sqrtf(Kf * smt) * e.asq);    // Y_s = yI * sum_k xi_k   (data.py:520)
+  const float cT = e.asq * sqrtf(tmt / Kf);
+  const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq);    // Y_T (data.py:917)
+  if (wv == 0) {
+    sh.tau[lane] = s;
+    sh.cmul[lane] = cI;
+  }
+  __syncthreads();  // xsh ready
+
+  // ---------------- phase 1: K-step Euler–Maruyama rollouts
+  float ST[8][4];
+  float gst[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int j = wv + 4 * c;  // terminal dim-blocks of this wave
+    ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
+    if (TERM && j < nb) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      for (int k = 0; k < a.K; ++k) {
+        const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
+        s0 += z.a;
+        s1 += z.b;
+        s2 += z.c;
+        s3 += z.d;
+      }
+      ST[c][0] = s0 * BM_SCALE;
+      ST[c][1] = s1 * BM_SCALE;
+      ST[c][2] = s2 * BM_SCALE;
+      ST[c][3] = s3 * BM_SCALE;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        if (d < nx) Eq<KIND>::gstat(e, d, fmaf(cT, ST[c][q], sh.xsh[d]), gst);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
+    if (j < nb) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      if (INTG) {
+        for (int k = 0; k < a.K; ++k) {
+          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
+          s0 += z.a;
+          s1 += z.b;
+          s2 += z.c;
+          s3 += z.d;
+        }
+      }
+      const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        sh.S[d * SS + lane] = d < nx ? sv[q] : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = gst[c];
+  __syncthreads();
+  float gT = 0.f;
+  if (TERM) {
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      gst[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
+                sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
+    gT = Eq<KIND>::gfin(e, gst);
+  }
+  const float ap = TERM ? gT - g_x : 0.f;  // (g(X_T) - g(x)) (data.py:923)
+
+  // ---------------- phase 2: u, grad u at (s, X_s) and f
+  float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
+  if (!ZERO && INTG) mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
+  {
+    const int pp = 16 * wv + (lane & 15);
+    if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
+  }
+  __syncthreads();
+
+  // ---------------- phase 3: per-path contributions -> per-block partial slab
+  const float bp = sh.bsh[lane];
+  // partial slab layout [point][2F][block]: the reduce kernel reads each column's blocks contiguously
+  float* out = a.partial + (size_t)i * 2 * F * a.nbp + blk;
+  const int nbs = a.nbp;
+  if (wv == 0) {
+    const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
+    const float s1 = wave_sum(c0), s2 = wave_sum(c0 * c0);
+    if (lane == 0) {
+      out[0] = s1;
+      out[(size_t)F * nbs] = s2;
+    }
+  }
+  const float aY = ap * yT, bY = bp * yI;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int j = wv + 4 * c;
+    if (j < nb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        if (d < nx) {
+          const float v = fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]);
+          const float s1 = wave_sum(v), s2 = wave_sum(v * v);
+          if (lane == 0) {
+            out[(size_t)(1 + d) * nbs] = s1;
+            out[(size_t)(F + 1 + d) * nbs] = s2;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Canonical fixed-order sum of `cnt` values (stride `stride`): zero-pad to a power of two
+// P2 >= 64 and add as a perfect binary tree in index order.  One wave per column: each lane
+// first sums its q = P2/64 consecutive values pairwise in registers, then the 64 lane values
+// are combined by an xor butterfly, whose every level adds aligned neighbours — the same tree.
+// Splitting the values over G ranks (G and cnt powers of two) and combining the rank results
+// with the same function therefore reproduces the single-call sum bit for bit.
+__device__ __forceinline__ float tree_sum(const float* __restrict__ p, int cnt, size_t stride) {
+  const int lane = threadIdx.x & 63;
+  int p2 = 64;
+  while (p2 < cnt) p2 <<= 1;
+  const int q = p2 >> 6;  // values per lane (<= 16)
+  float v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int b = lane * q + j;
+    v[j] = (j < q && b < cnt) ? p[(size_t)b * stride] : 0.f;
+  }
+#pragma unroll
+  for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+    for (int j = 0; j < 16; j += 2 * w)
+      if (j + w < q) v[j] = v[j] + v[j + w];
+  float s = v[0];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float other = __shfl_xor(s, o, 64);
+    s = (lane & o) ? other + s : s + other;  // always (left + right): identical on both lanes
+  }
+  return s;
+}
+
+// partial [n][2F][nbp] -> moments [n][2F] (and, if y != nullptr, the finalized labels).
+__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
+                                                float* __restrict__ moments, const float* __restrict__ gx,
+                                                float invM, int add_g, float bound, float* __restrict__ y) {
+  const int i = blockIdx.x;
+  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (c >= 2 * F) return;
+  const float s = tree_sum(partial + ((size_t)i * 2 * F + c) * nbp, nbp, 1);
+  if ((threadIdx.x & 63) == 0) {
+    moments[(size_t)i * 2 * F + c] = s;
+    if (y && c < F) {
+      float v = s * invM;
+      if (c == 0 && add_g) v += gx[i];
+      y[(size_t)i * F + c] = fminf(fmaxf(v, -bound), bound);
+    }
+  }
+}
+
+// parts [G][len] -> out [len]
+__global__ __launch_bounds__(256) void k_reduce_parts(const float* __restrict__ parts, int G, int len,
+                                                      float* __restrict__ out) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= len) return;
+  const float s = tree_sum(parts + c, G, (size_t)len);
+  if ((threadIdx.x & 63) == 0) out[c] = s;
+}
+
+__global__ void k_finalize(const float* moments, const float* gx, int n, int F, float invM, int add_g, float bound,
+                           float* y) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * F) return;
+  const int i = gid / F, c = gid - i * F;
+  float v = moments[(size_t)i * 2 * F + c] * invM;
+  if (c == 0 && add_g) v += gx[i];
+  y[gid] = fminf(fmaxf(v, -bound), bound);
+}
+
+}  // namespace dpi
+
+// ================================================================================ C-ABI
+using namespace dpi;
+
+struct dpi_problem_s {
+  EqDev e;
+  float alpha_init_sqrt;
+  std::vector<void*> dev;
+};
+
+struct dpi_net_s {
+  NetDev d;
+  void* blob = nullptr;
+  int n_in = 0;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                                    \
+  do {                                                                                               \
+    hipError_t _e = (x);                                                                             \
+    if (_e != hipSuccess) return fail(DPI_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename T>
+static int upload(dpi_problem_s* p, const std::vector<T>& v, const T** out) {
+  void* d = nullptr;
+  HIPCHK(hipMalloc(&d, v.size() * sizeof(T) + 16));
+  HIPCHK(hipMemcpy(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  p->dev.push_back(d);
+  *out = reinterpret_cast<const T*>(d);
+  return 0;
+}
+
+extern "C" {
+
+int dpi_abi_version(void) { return DPI_ABI_VERSION; }
+
+int dpi_last_error(char* buf, size_t len) {
+  if (buf && len) {
+    std::strncpy(buf, g_err.c_str(), len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)g_err.size();
+}
+
+static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
+  auto* p = new dpi_problem_s();
+  std::memset(&p->e, 0, sizeof(p->e));
+  p->e.kind = kind;
+  p->e.nx = nx;
+  p->e.T = (float)T;
+  p->e.alpha = (float)alpha;
+  p->e.asq = (float)std::sqrt(alpha);
+  p->alpha_init_sqrt = 0.f;
+  return p;
+}
+
+int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out) {
+  if (!out || nx < 1 || nx > NXP_MAX || !(alpha > 0)) return fail(DPI_ERR_ARG, "cha: bad arguments");
+  auto* p = new_problem(DPI_EQ_CHA, nx, alpha, T);
+  const double kp = k / std::sqrt((double)nx);  // equations.py:285
+  const double k_alpha_d = kp * alpha * nx;
+  p->e.cha_k = (float)kp;
+  p->e.cha_C = (float)((2.0 + kp * k_alpha_d) / (2.0 * k_alpha_d));
+  *out = p;
+  return 0;
+}
+
+int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale, int n_comp,
+                          const double* mean, const double* var_diag, const double* pi, dpi_problem* out) {
+  if (!out || nx < 1 || nx > NXP_MAX || n_comp < 1 || n_comp > NSG || !mean || !var_diag || !pi)
+    return fail(DPI_ERR_ARG, "ou: bad arguments (1 <= n_comp <= 8, nx <= 128)");
+  auto* p = new_problem(DPI_EQ_OU, nx, alpha, T);
+  p->e.ou_theta = (float)theta;
+  p->e.ou_mu = (float)mu;
+  p->e.ou_d = (float)nx;
+  p->e.ncomp = n_comp;
+  p->alpha_init_sqrt = (float)std::sqrt(alpha_scale * alpha);
+  std::vector<float> m(n_comp * nx), iv(n_comp * nx), lc(n_comp);
+  const double log2pi = std::log(2.0 * M_PI);
+  for (int c = 0; c < n_comp; ++c) {
+    double logdet = 0;
+    for (int d = 0; d < nx; ++d) {
+      m[c * nx + d] = (float)mean[c * nx + d];
+      iv[c * nx + d] = (float)(1.0 / var_diag[c * nx + d]);
+      logdet += std::log(var_diag[c * nx + d]);
+    }
+    lc[c] = (float)(std::log(pi[c]) - 0.5 * (nx * log2pi + logdet));
+  }
+  int rc;
+  if ((rc = upload(p, m, &p->e.mean)) || (rc = upload(p, iv, &p->e.ivar)) || (rc = upload(p, lc, &p->e.logc))) {
+    delete p;
+    return rc;
+  }
+  *out = p;
+  return 0;
+}
+
+int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
+                           dpi_problem* out) {
+  return fail(DPI_ERR_UNSUPPORTED, "GBMEquationComplexExact: not yet supported by this build");
+}
+
+int dpi_problem_destroy(dpi_problem p) {
+  if (!p) return 0;
+  for (void* d : p->dev) (void)hipFree(d);
+  delete p;
+  return 0;
+}
+
+int dpi_net_create_zero(dpi_net* out) {
+  if (!out) return fail(DPI_ERR_ARG, "null out");
+  auto* n = new dpi_net_s();
+  std::memset(&n->d, 0, sizeof(n->d));
+  n->d.kind = 0;
+  *out = n;
+  return 0;
+}
+
+int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params, size_t n_params,
+                       dpi_net* out) {
+  if (!out || !widths || !params || n_in < 2 || n_in - 1 > NXP_MAX || n_hidden < 1 || n_hidden > 4)
+    return fail(DPI_ERR_ARG, "mlp: bad arguments");
+  if (act != DPI_ACT_ELU) return fail(DPI_ERR_UNSUPPORTED, "mlp: only ELU activations are supported");
+  const int H = widths[0];
+  for (int l = 1; l < n_hidden; ++l)
+    if (widths[l] != H) return fail(DPI_ERR_UNSUPPORTED, "mlp: hidden widths must be equal");
+  if (!(H == 16 || H == 32 || H == 64 || H == 128)) return fail(DPI_ERR_UNSUPPORTED, "mlp: width must be 16/32/64/128");
+  const int nx = n_in - 1, nxp = (nx + 15) & ~15, L = n_hidden;
+  const size_t expect = (size_t)H * n_in + H + (size_t)(L - 1) * (H * H + H) + H + 1;
+  if (n_params != expect) return fail(DPI_ERR_ARG, "mlp: parameter count mismatch");
+  // host-side repack
+  std::vector<float> blob;
+  auto take = [&](size_t cnt) {
+    size_t off = blob.size();
+    blob.resize(off + ((cnt + 3) & ~size_t(3)), 0.f);
+    return off;
+  };
+  const float* W0 = params;
+  const float* b0 = W0 + (size_t)H * n_in;
+  const size_t oW1x = take((size_t)H * nxp), ow1t = take(H), ob1 = take(H), oc1 = take(H), oW1xT = take((size_t)nxp * H);
+  for (int h = 0; h < H; ++h) {
+    double cs = 0;
+    for (int d = 0; d < nx; ++d) {
+      const float w = W0[(size_t)h * n_in + 1 + d];
+      blob[oW1x + (size_t)h * nxp + d] = w;
+      blob[oW1xT + (size_t)d * H + h] = w;
+      cs += w;
+    }
+    blob[ow1t + h] = W0[(size_t)h * n_in];
+    blob[ob1 + h] = b0[h];
+    blob[oc1 + h] = (float)cs;
+  }
+  const float* cur = b0 + H;
+  size_t oW[4] = {0}, oWT[4] = {0}, ob[4] = {0};
+  for (int l = 1; l < L; ++l) {
+    oW[l] = take((size_t)H * H);
+    oWT[l] = take((size_t)H * H);
+    ob[l] = take(H);
+    for (int r = 0; r < H; ++r)
+      for (int c = 0; c < H; ++c) {
+        blob[oW[l] + (size_t)r * H + c] = cur[(size_t)r * H + c];
+        blob[oWT[l] + (size_t)c * H + r] = cur[(size_t)r * H + c];
+      }
+    cur += (size_t)H * H;
+    for (int h = 0; h < H; ++h) blob[ob[l] + h] = cur[h];
+    cur += H;
+  }
+  const size_t owout = take(H);
+  for (int h = 0; h < H; ++h) blob[owout + h] = cur[h];
+  const float bout = cur[H];
+  auto* n = new dpi_net_s();
+  std::memset(&n->d, 0, sizeof(n->d));
+  void* d = nullptr;
+  if (hipMalloc(&d, blob.size() * sizeof(float)) != hipSuccess) {
+    delete n;
+    return fail(DPI_ERR_HIP, "mlp: hipMalloc failed");
+  }
+  if (hipMemcpy(d, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    delete n;
+    return fail(DPI_ERR_HIP, "mlp: hipMemcpy failed");
+  }
+  const float* base = reinterpret_cast<const float*>(d);
+  n->blob = d;
+  n->n_in = n_in;
+  n->d.kind = 1;
+  n->d.H = H;
+  n->d.L = L;
+  n->d.nxp = nxp;
+  n->d.W1x = base + oW1x;
+  n->d.w1t = base + ow1t;
+  n->d.b1 = base + ob1;
+  n->d.c1 = base + oc1;
+  n->d.W1xT = base + oW1xT;
+  for (int l = 1; l < L; ++l) {
+    n->d.W[l] = base + oW[l];
+    n->d.WT[l] = base + oWT[l];
+    n->d.b[l] = base + ob[l];
+  }
+  n->d.wout = base + owout;
+  n->d.bout = bout;
+  *out = n;
+  return 0;
+}
+
+int dpi_net_destroy(dpi_net net) {
+  if (!net) return 0;
+  if (net->blob) (void)hipFree(net->blob);
+  delete net;
+  return 0;
+}
+
+}  // extern "C"
+
+// Workspace: gx[n] | fb[n] | bx[n][H] | partial[n][nbp][2][F]   (256-B aligned pieces)
+struct WsLayout {
+  size_t gx, fb, bx, partial, total;
+};
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
+  WsLayout w;
+  const int H = (net && net->d.kind) ? net->d.H : 0;
+  const size_t nbp = (size_t)(M + P - 1) / P;
+  w.gx = 0;
+  w.fb = al256((size_t)n * 4);
+  w.bx = w.fb + al256((size_t)n * 4);
+  w.partial = w.bx + al256((size_t)n * H * 4);
+  w.total = w.partial + (size_t)n * nbp * 2 * F * 4;
+  return w;
+}
+
+extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) {
+  if (!p || n < 0 || M < 0) return 0;
+  return ws_layout(net, n, M, 1 + p->e.nx).total;
+}
+
+extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
+                      float* tx, void* stream) {
+  if (!p || !tx || n < 0 || epoch > 0xFFFFFFu) return fail(DPI_ERR_ARG, "sample_points: bad arguments");
+  if (n == 0) return 0;
+  const int nb = (p->e.nx + 3) >> 2;
+  const int total = n * nb;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t c3t = DPI_TAG_T | (epoch << 8), c3x0 = DPI_TAG_X0 | (epoch << 8), c3x = DPI_TAG_X | (epoch << 8);
+  dim3 grid((total + 255) / 256), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->e.kind) {
+    case DPI_EQ_CHA:
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_CHA>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
+                         eps, p->alpha_init_sqrt, tx);
+      break;
+    case DPI_EQ_OU:
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_OU>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
+                         eps, p->alpha_init_sqrt, tx);
+      break;
+    default:
+      return fail(DPI_ERR_UNSUPPORTED, "sample_points: equation kind");
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ---- dispatch over (equation, network shape)
+struct Launch {
+  bool baseline;
+  const float* tx;
+  int n;
+  float *gx, *fb, *bx;
+  const PathArgs* a;
+  int nblocks;
+  hipStream_t st;
+};
+
+template <int KIND, int H, int L, bool Z>
+static void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if (q.baseline)
+    hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTH), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+                       q.bx);
+  else
+    hipLaunchKernelGGL((k_paths<KIND, H, L, Z>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+}
+
+template <int KIND>
+static bool dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if (net->d.kind == 0) {
+    do_launch<KIND, 16, 1, true>(p, net, q);
+    return true;
+  }
+  if (q.baseline) {  // the baseline kernel is shape-generic
+    do_launch<KIND, 16, 1, false>(p, net, q);
+    return true;
+  }
+  const int H = net->d.H, L = net->d.L;
+#define DPI_SHAPE(HH, LL)                      \
+  if (H == HH && L == LL) {                    \
+    do_launch<KIND, HH, LL, false>(p, net, q); \
+    return true;                               \
+  }
+  DPI_SHAPE(128, 4)
+  DPI_SHAPE(128, 3)
+  DPI_SHAPE(128, 2)
+  DPI_SHAPE(64, 3)
+  DPI_SHAPE(64, 2)
+  DPI_SHAPE(32, 2)
+  DPI_SHAPE(16, 1)
+  DPI_SHAPE(16, 2)
+  DPI_SHAPE(16, 3)
+#undef DPI_SHAPE
+  return false;
+}
+
+static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  switch (p->e.kind) {
+    case DPI_EQ_CHA:
+      return dispatch<DPI_EQ_CHA>(p, net, q);
+    case DPI_EQ_OU:
+      return dispatch<DPI_EQ_OU>(p, net, q);
+    default:
+      return false;
+  }
+}
+
+static int check_pair(dpi_problem p, dpi_net net);
+extern "C" {
+static int check_pair(dpi_problem p, dpi_net net) {
+  if (!p || !net) return fail(DPI_ERR_ARG, "null problem or net");
+  if (net->d.kind && net->n_in != 1 + p->e.nx) return fail(DPI_ERR_ARG, "net input width != 1 + nx");
+  if (net->d.kind && net->d.nxp > NXP_MAX) return fail(DPI_ERR_ARG, "nx too large");
+  return 0;
+}
+
+int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (!tx || !ws || n < 0) return fail(DPI_ERR_ARG, "point_baseline: bad arguments");
+  if (n == 0) return 0;
+  const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
+  if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  char* b = (char*)ws;
+  Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), nullptr, 0, (hipStream_t)stream};
+  if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "point_baseline: unsupported equation/network shape");
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                        uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
+                        void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (!tx || !ws || !moments || n < 0 || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
+      (m_begin % P) || (m_end % P) || !(flags & DPI_BOTH) || (flags & ~DPI_BOTH) || epoch > 0xFFFFFFu)
+    return fail(DPI_ERR_ARG, "label_moments: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
+  if (n == 0) return 0;
+  const int F = 1 + p->e.nx;
+  const int nbp = (m_end - m_begin) / P;
+  if (nbp > 1024) return fail(DPI_ERR_ARG, "label_moments: at most 1024 x 64 paths per call");
+  const WsLayout w = ws_layout(net, n, M, F);
+  if (ws_bytes < w.total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  char* b = (char*)ws;
+  float* partial = (float*)(b + w.partial);
+  PathArgs a;
+  a.tx = tx;
+  a.gx = (const float*)(b + w.gx);
+  a.fb = (const float*)(b + w.fb);
+  a.bx = (const float*)(b + w.bx);
+  a.partial = partial;
+  a.n = n;
+  a.nbp = nbp;
+  a.m_begin = m_begin;
+  a.K = K;
+  a.flags = flags;
+  a.k0 = (uint32_t)seed;
+  a.k1 = (uint32_t)(seed >> 32);
+  a.c3t = DPI_TAG_TERM | (epoch << 8);
+  a.c3s = DPI_TAG_S | (epoch << 8);
+  a.c3i = DPI_TAG_INT | (epoch << 8);
+  a.point_base = point_base;
+  hipStream_t st = (hipStream_t)stream;
+  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, &a, n * nbp, st};
+  if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
+                     (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,
+                      uint32_t point_base, int m_begin, int m_end, int flags, float* moments, void* ws,
+                      size_t ws_bytes, void* stream) {
+  return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, moments, ws, ws_bytes,
+                      stream, nullptr, 0.f);
+}
+
+int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, void* stream) {
+  if (!parts || !out || n_parts < 1 || n < 0 || nx < 1) return fail(DPI_ERR_ARG, "moments_reduce: bad arguments");
+  if (n == 0) return 0;
+  if (n_parts > 1024) return fail(DPI_ERR_ARG, "moments_reduce: at most 1024 parts");
+  const int len = n * 2 * (1 + nx);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_reduce_parts, dim3((len + 3) / 4), dim3(256), 0, st, (const float*)parts, n_parts, len, out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int dpi_label_finalize(dpi_problem p, const float* moments, int n, int M, int flags, float sample_bound, float* y,
+                       const void* ws, size_t ws_bytes, void* stream) {
+  if (!p || !moments || !y || !ws || n < 0 || M < 1 || ws_bytes < (size_t)n * 4)
+    return fail(DPI_ERR_ARG, "label_finalize: bad arguments");
+  if (n == 0) return 0;
+  const int F = 1 + p->e.nx;
+  hipLaunchKernelGGL(k_finalize, dim3((n * F + 255) / 256), dim3(256), 0, (hipStream_t)stream, moments,
+                     (const float*)ws, n, F, 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, sample_bound, y);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                                uint32_t epoch, uint32_t point_base, int flags, float sample_bound, float* y,
+                                float* moments, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (n == 0) return 0;
+  const int F = 1 + p->e.nx;
+  const WsLayout w = ws_layout(net, n, M, F);
+  if (!ws || ws_bytes < w.total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  if (!moments) return fail(DPI_ERR_ARG, "generate_with_gradients: moments buffer (n*2*(1+nx) floats) required");
+  if ((rc = dpi_point_baseline(p, net, tx, n, ws, ws_bytes, stream))) return rc;
+  if (!y) return fail(DPI_ERR_ARG, "generate_with_gradients: null y");
+  // moments and labels come out of the same block-reduce launch
+  return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, moments, ws, ws_bytes, stream, y,
+                      sample_bound);
+}
+
+}  // extern "C"

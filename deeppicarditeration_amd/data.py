@@ -1,0 +1,195 @@
+"""DPI label generation on MI355X — the drop-in for the reference's
+`OnlineDataGenerator` (picard/data.py:369-1223) behind the `batch_data_generator` boundary
+(`IterableDatasetWithInternalBatch`, picard/dataset.py:27, :112).
+
+Same constructor arguments and method names as the reference; every label is computed by
+the HIP kernels of libdpi_hip.so through the C-ABI (include/dpi.h).  There is no eager /
+CPU fallback: a missing library or an unsupported configuration raises.
+
+Differences from the reference, by design:
+- noise is counter-based Philox4x32-10 keyed by (seed, epoch = Picard iteration, point index,
+  MC index, EM step) instead of torch's unseeded global RNG (the reference sets no seed), so
+  labels are reproducible and independent of how paths are split over GPUs;
+- each forward path is a K-step Euler–Maruyama rollout (`n_euler_steps`, default 50); for the
+  zero-drift SDE of every shipped equation this equals the reference's one-jump sampler in
+  distribution, and pathwise when the reference is fed xi_eff = sum_k xi_k / sqrt(K);
+- tensors are fp32 on the GPU (the YAMLs say DATA.FLOAT: double; parity is measured against
+  the fp64 reference, tests/test_gpu_parity.py).
+"""
+from typing import Union
+
+import torch
+
+from . import _lib
+from .equations import Equation, OUProcessEquation, SimpleDiffusionEquation
+from .solution import DeviceNet
+
+
+def _ptr(t):
+    return _lib.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    return _lib.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class OnlineDataGenerator:
+    """picard/data.py:369-431 (constructor), :211-223 / :1208-1218 (label entry points)."""
+
+    do_internal_batching = True
+
+    def __init__(self, equation: Equation, solution: torch.nn.Module, N: int, i: int, *,
+                 device: Union[str, torch.device] = "cuda", t_always_uniform=False, n_estimate_terminal=1,
+                 n_estimate_integral=1, hessian_approximation=None, sample_bound=None, estimate_terminal="OU_ByGx",
+                 estimate_integral="OU_Simple", estimate_delta_t=0.0, n_euler_steps: int = 50, seed: int = 0,
+                 epoch: int = None):
+        if not (isinstance(equation, SimpleDiffusionEquation) or isinstance(equation, OUProcessEquation)):
+            raise AssertionError("Currently only SimpleDiffusionEquation and OUProcessEquation are supported")  # :426-429
+        if equation.nu != 1:
+            raise AssertionError("Currently only nu=1 is supported")
+        if not t_always_uniform:
+            raise NotImplementedError("t_always_uniform=False (product-of-uniforms t sampler) is not built yet")
+        if estimate_delta_t and estimate_delta_t > 0:
+            raise NotImplementedError("TD estimators (ESTIMATE_DELTA_T > 0) are out of scope for this build")
+        method = getattr(hessian_approximation, "method", None) if hessian_approximation is not None else None
+        if method is not None:
+            raise NotImplementedError(f"hessian approximation {method!r} is not built yet")
+        self.equation = equation
+        self.solution = solution
+        self.N, self.i = N, i
+        self.T = float(equation.T)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the HIP label generator runs on a GPU device ('cuda' on ROCm)")
+        self.n_estimate_terminal = int(n_estimate_terminal)
+        self.n_estimate_integral = int(n_estimate_integral)
+        for m in (self.n_estimate_terminal, self.n_estimate_integral):
+            if m % _lib.DPI_PATH_BLOCK:
+                raise ValueError(f"Monte-Carlo sample counts must be multiples of {_lib.DPI_PATH_BLOCK} (got {m})")
+        self.sample_bound = float("inf") if sample_bound is None else float(sample_bound)
+        self.estimate_terminal_type = estimate_terminal
+        self.estimate_integral_type = estimate_integral
+        # data.py:134-137
+        self.eps = 0.01 if ("ByGx" in (estimate_terminal or "") or "Joint" in (estimate_integral or "")) else 0.0
+        self.K = int(n_euler_steps)
+        if self.K < 1:
+            raise ValueError("n_euler_steps must be >= 1")
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.epoch = int(i if epoch is None else epoch) & 0xFFFFFF
+        self.point_base = 0
+        self.lib = _lib.load()
+        for p in solution.parameters():  # data.py:409-412
+            p.requires_grad = False
+        solution.eval()
+        self.net = DeviceNet.from_module(solution, 1 + equation.nx)
+        self.problem = equation.dpi_problem()
+        self._ws = None
+
+    # ------------------------------------------------------------------ buffers
+    def _workspace(self, n, M):
+        need = self.lib.dpi_workspace_bytes(self.problem, self.net.handle, n, M)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _take_points(self, n):
+        base = self.point_base
+        self.point_base = (self.point_base + n) & 0xFFFFFFFF
+        return base
+
+    # ------------------------------------------------------------------ reference entry points
+    def sample_t_and_x(self, n_batch, point_base=None):
+        """sample_t_always_uniform + equation.sample_x (data.py:161-167, :211-217): tx (n, 1+nx)."""
+        tx = torch.empty(n_batch, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        pb = self._take_points(n_batch) if point_base is None else point_base
+        _lib.check(self.lib.dpi_sample_points(self.problem, n_batch, self.seed, self.epoch, pb, self.eps, _ptr(tx),
+                                              _stream(self.device)), "dpi_sample_points")
+        return tx, pb
+
+    def sample_with_gradients(self, n_batch):
+        """data.py:211-223: (tx, clip(u_ux)) with u_ux (n, 1+nx)."""
+        tx, pb = self.sample_t_and_x(n_batch)
+        return tx, self._generate(tx, pb, _lib.DPI_BOTH)
+
+    def generate_with_gradients(self, tx, point_base=None):
+        """data.py:1208-1218: terminal + integral estimators at given points (no clip)."""
+        pb = self._take_points(tx.shape[0]) if point_base is None else point_base
+        return self._generate(self._as_points(tx), pb, _lib.DPI_BOTH, bound=float("inf"))
+
+    def estimate_terminal_with_gradients(self, tx, point_base=None):
+        """data.py:899-926."""
+        pb = self._take_points(tx.shape[0]) if point_base is None else point_base
+        return self._generate(self._as_points(tx), pb, _lib.DPI_TERMINAL, bound=float("inf"))
+
+    def estimate_integral_with_gradients(self, tx, point_base=None):
+        """data.py:471-527."""
+        pb = self._take_points(tx.shape[0]) if point_base is None else point_base
+        return self._generate(self._as_points(tx), pb, _lib.DPI_INTEGRAL, bound=float("inf"))
+
+    def dataset_with_gradients(self, n_total, n_batch_buffer, batch_size):
+        """data.py:291-297: the reference's buffered iterable dataset over sample_with_gradients."""
+        from .dataset import IterableDatasetWithInternalBatch
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
+
+    # ------------------------------------------------------------------ moments (sharding building blocks)
+    def point_baseline(self, tx):
+        n = tx.shape[0]
+        M = max(self.n_estimate_terminal, self.n_estimate_integral)
+        ws = self._workspace(n, M)
+        _lib.check(self.lib.dpi_point_baseline(self.problem, self.net.handle, _ptr(tx), n, _ptr(ws), ws.numel(),
+                                               _stream(self.device)), "dpi_point_baseline")
+        return ws
+
+    def label_moments(self, tx, point_base, M, m_begin, m_end, flags, ws):
+        """Sum / sum-of-squares of per-path contributions over m in [m_begin, m_end): (n, 2, 1+nx)."""
+        n = tx.shape[0]
+        mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.dpi_label_moments(self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed,
+                                              self.epoch, point_base, m_begin, m_end, flags, _ptr(mom), _ptr(ws),
+                                              ws.numel(), _stream(self.device)), "dpi_label_moments")
+        return mom
+
+    def finalize(self, moments, M, flags, ws, bound=None):
+        n = moments.shape[0]
+        y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        b = self.sample_bound if bound is None else bound
+        _lib.check(self.lib.dpi_label_finalize(self.problem, _ptr(moments), n, M, flags, b, _ptr(y), _ptr(ws),
+                                               ws.numel(), _stream(self.device)), "dpi_label_finalize")
+        return y
+
+    def moments_reduce(self, parts):
+        """(G, n, 2, 1+nx) per-rank moments -> (n, 2, 1+nx), fixed pairwise order (parts is scratch)."""
+        parts = parts.contiguous()
+        G, n = parts.shape[0], parts.shape[1]
+        out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
+        _lib.check(self.lib.dpi_moments_reduce(_ptr(parts), G, n, self.equation.nx, _ptr(out), _stream(self.device)),
+                   "dpi_moments_reduce")
+        return out
+
+    # ------------------------------------------------------------------ internals
+    def _as_points(self, tx):
+        if tx.device != self.device or tx.dtype != torch.float32 or not tx.is_contiguous():
+            tx = tx.to(device=self.device, dtype=torch.float32).contiguous()
+        return tx
+
+    def _generate(self, tx, pb, flags, bound=None):
+        MT, MI = self.n_estimate_terminal, self.n_estimate_integral
+        if MT == MI or flags != _lib.DPI_BOTH:
+            # one C-ABI call: baseline + fused rollout/label kernel + block reduce/finalize
+            M = MT if flags == _lib.DPI_TERMINAL else MI
+            n = tx.shape[0]
+            ws = self._workspace(n, max(MT, MI))
+            y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+            self.last_moments = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+            b = self.sample_bound if bound is None else bound
+            _lib.check(self.lib.dpi_generate_with_gradients(
+                self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, flags, b, _ptr(y),
+                _ptr(self.last_moments), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_generate_with_gradients")
+            return y
+        ws = self.point_baseline(tx)
+        yT = self.finalize(self.label_moments(tx, pb, MT, 0, MT, _lib.DPI_TERMINAL, ws), MT, _lib.DPI_TERMINAL, ws,
+                           float("inf"))
+        yI = self.finalize(self.label_moments(tx, pb, MI, 0, MI, _lib.DPI_INTEGRAL, ws), MI, _lib.DPI_INTEGRAL, ws,
+                           float("inf"))
+        b = self.sample_bound if bound is None else bound
+        return torch.clamp(yT + yI, -b, b)

@@ -1,0 +1,53 @@
+"""Monte-Carlo sharding of the label path across GPUs (one process per GPU, torch.distributed
+over RCCL/xGMI).
+
+Every path-label is independent and a label is a mean over MC indices m, so rank r of G owns
+m in [r M/G, (r+1) M/G) for all points.  Noise counters are global (seed, epoch, point, m, step),
+so each path sees the same noise for any G, and the collocation points are sampled identically
+on every rank from the same counters (no broadcast).  The one exchange is an all-gather of the
+per-rank label moments (n, 2, 1+nx) fp32 — 2 x 16 x 101 x 4 B = 12.9 kB per rank at config 2,
+414 kB in total at config 4 — followed by dpi_moments_reduce, the same fixed pairwise tree the
+kernel uses over 64-path blocks.  With M/(64 G) a power of two the labels are bit-identical for
+G = 1, 2, 4, 8.  (The reference has no collective: SURVEY.md §2 rows 18-19.)
+"""
+import torch
+
+
+class ShardedLabeler:
+    def __init__(self, gen, rank=0, world=1, group=None):
+        self.gen = gen
+        self.rank = rank
+        self.world = world
+        self.group = group
+
+    def shard(self, M):
+        blk = 64
+        if M % (blk * self.world):
+            raise ValueError(f"M={M} must be a multiple of 64 x world ({self.world})")
+        per = M // self.world
+        return self.rank * per, (self.rank + 1) * per
+
+    def gather_moments(self, mom):
+        if self.world == 1:
+            return mom
+        import torch.distributed as dist
+        parts = torch.empty((self.world,) + tuple(mom.shape), dtype=mom.dtype, device=mom.device)
+        dist.all_gather_into_tensor(parts, mom.contiguous(), group=self.group)
+        return self.gen.moments_reduce(parts)
+
+    def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
+        """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""
+        from . import _lib
+        flags = _lib.DPI_BOTH if flags is None else flags
+        M = self.gen.n_estimate_integral
+        if self.gen.n_estimate_terminal != M:
+            raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
+        ws = self.gen.point_baseline(tx)
+        m0, m1 = self.shard(M)
+        if on_moments_begin:
+            on_moments_begin()
+        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags, ws)
+        if on_moments_end:
+            on_moments_end()
+        mom = self.gather_moments(mom)
+        return self.gen.finalize(mom, M, flags, ws)

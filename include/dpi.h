@@ -1,0 +1,137 @@
+/*
+ * dpi.h — C-ABI of the MI355X-native DPI label-generation hot path (libdpi_hip.so).
+ *
+ * Plain pointers and sizes only; no torch types.  Every device pointer is caller-owned
+ * (e.g. a torch-ROCm tensor's data_ptr()); the library never frees caller memory.  Calls are
+ * stream-ordered on `stream` (a hipStream_t; NULL = default stream) and never synchronise
+ * the device, so they can be captured into a hipGraph.  Return 0 on success or a negative
+ * DPI_ERR_* code; dpi_last_error() returns the thread-local message.  No C++ exception
+ * crosses the ABI.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo):
+ *   dpi_problem_create_cha   picard/equations.py:266-338  Cha(nx, alpha, k, T)
+ *   dpi_problem_create_ou    picard/equations.py:489-714  OUProcessEquation(...) + utils.py:792-914 GMM
+ *   dpi_problem_create_gbm   picard/equations.py:388-486  GBMEquationComplexExact(nx, alpha, T)
+ *   dpi_net_create_zero      picard/solution.py:330-337   ZeroSolution (iteration 1)
+ *   dpi_net_create_mlp       picard/solution.py:123-135   construct_mlp (state-dict order)
+ *   dpi_sample_points        picard/data.py:161-167, :211-217  sample_t_always_uniform + equation.sample_x
+ *   dpi_point_baseline       picard/data.py:506-518, :918-920  g(x) and get_f(..., baseline_repeat=M)
+ *   dpi_label_moments        picard/data.py:899-926 + :471-527 (+ :1226-1325 get_f) summed over MC paths
+ *   dpi_label_finalize       picard/data.py:924-926, :525-526, :222  mean over M, + g(x), clip
+ *   dpi_generate_with_gradients  picard/data.py:1208-1218 (baseline + moments + finalize)
+ *   dpi_moments_reduce       (no reference counterpart: fixed-order combine of per-rank moments)
+ */
+#ifndef DPI_H_
+#define DPI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPI_ABI_VERSION 1
+
+/* error codes */
+#define DPI_OK 0
+#define DPI_ERR_ARG (-1)
+#define DPI_ERR_UNSUPPORTED (-2)
+#define DPI_ERR_HIP (-3)
+#define DPI_ERR_WORKSPACE (-4)
+
+/* Philox stream tags: counter word c3 = tag | (epoch << 8) (see csrc/dpi_rng.h) */
+#define DPI_TAG_T 1
+#define DPI_TAG_X0 2
+#define DPI_TAG_X 3
+#define DPI_TAG_TERM 4
+#define DPI_TAG_S 5
+#define DPI_TAG_INT 6
+#define DPI_TAG_SDGD 7
+#define DPI_TAG_HTERM 8
+#define DPI_TAG_HINT 9
+
+/* equation kinds */
+#define DPI_EQ_CHA 1
+#define DPI_EQ_OU 2
+#define DPI_EQ_GBM 3
+
+/* activations */
+#define DPI_ACT_ELU 1
+
+/* estimator selection (dpi_label_moments / finalize flags) */
+#define DPI_TERMINAL 1 /* estimate_terminal_with_gradients (data.py:899-926) */
+#define DPI_INTEGRAL 2 /* estimate_integral_with_gradients (data.py:471-527) */
+#define DPI_BOTH 3     /* generate_with_gradients (data.py:1208-1218) */
+
+/* Monte-Carlo paths per workgroup: m ranges are multiples of this. */
+#define DPI_PATH_BLOCK 64
+
+typedef struct dpi_problem_s* dpi_problem;
+typedef struct dpi_net_s* dpi_net;
+
+int dpi_abi_version(void);
+/* Copies the calling thread's last error message (NUL-terminated); returns its length. */
+int dpi_last_error(char* buf, size_t len);
+
+/* --- problem plugins (host parameters copied to device; fp64 in, fp32 on device) --- */
+int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out);
+/* mean: (n_comp, nx); var_diag: (n_comp, nx) diagonal of each component covariance; pi: (n_comp) */
+int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale,
+                          int n_comp, const double* mean, const double* var_diag, const double* pi,
+                          dpi_problem* out);
+/* w: (n_nodes, 1+nx); v: (n_nodes) */
+int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
+                           dpi_problem* out);
+int dpi_problem_destroy(dpi_problem p);
+
+/* --- networks u(t, x): weights uploaded once per Picard iteration into a library handle --- */
+int dpi_net_create_zero(dpi_net* out);
+/* params: host fp32, torch state-dict order of construct_mlp(n_in, 1, widths, act):
+ *   W0 (widths[0] x n_in), b0, W1 (widths[1] x widths[0]), b1, ..., Wout (1 x widths[-1]), bout.
+ * Supported (width, n_hidden): all hidden widths equal, one of 16/32/64/128, n_hidden 1..4. */
+int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params,
+                       size_t n_params, dpi_net* out);
+int dpi_net_destroy(dpi_net net);
+
+/* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
+size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
+
+/* Draws 1-3 of sample_with_gradients: tx (n, 1+nx) fp32 device, t = (T-2eps)(1-U)+eps,
+ * x = x0 + sqrt(t) sqrt(alpha) xi.  Point i uses counter c2 = point_base + i. */
+int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
+                      float* tx, void* stream);
+
+/* Per-point baseline g(x), f(t, x, u, grad u) (+ network terms) into the workspace. */
+int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes,
+                       void* stream);
+
+/* Label moments over MC indices m in [m_begin, m_end) of M (both multiples of DPI_PATH_BLOCK)
+ * with K Euler–Maruyama steps per path.  moments (n, 2, 1+nx) fp32: [0] = sum of per-path
+ * contributions, [1] = sum of squares.  Summation order is fixed (pairwise over 64-path
+ * blocks), so results are bit-reproducible; ranges aligned to power-of-two block counts
+ * combine with dpi_moments_reduce bit-identically to a single call.  Requires
+ * dpi_point_baseline on the same workspace first. */
+int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                      uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
+                      void* ws, size_t ws_bytes, void* stream);
+
+/* parts: (n_parts, n, 2, 1+nx) -> out (n, 2, 1+nx) with the same pairwise tree as
+ * dpi_label_moments' block sum.  `parts` is read only. */
+int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, void* stream);
+
+/* y (n, 1+nx) = moments[:,0]/M + (g(x), 0...) [if DPI_TERMINAL], clipped to +-sample_bound. */
+int dpi_label_finalize(dpi_problem p, const float* moments, int n, int M, int flags, float sample_bound,
+                       float* y, const void* ws, size_t ws_bytes, void* stream);
+
+/* All of the above for m in [0, M): generate_with_gradients(tx) -> y (n, 1+nx); moments
+ * (n, 2, 1+nx) receives the label moments (required). */
+int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
+                                uint64_t seed, uint32_t epoch, uint32_t point_base, int flags,
+                                float sample_bound, float* y, float* moments, void* ws, size_t ws_bytes,
+                                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPI_H_ */

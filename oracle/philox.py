@@ -71,10 +71,15 @@ def uniform_oc(w):
     return ((np.asarray(w, np.uint32) >> np.uint32(8)).astype(np.float64) + 1.0) * TWO_M24
 
 
+TWO_M23 = 1.0 / 8388608.0
+
+
 def box_muller(wa, wb):
-    """Two normals from two words: r = sqrt(-2 ln u1), (r cos 2pi u2, r sin 2pi u2)."""
-    u1 = uniform_oc(wa)
-    u2 = uniform_co(wb)
+    """Two normals from two words (Box–Muller on 23-bit uniforms, csrc/dpi_rng.h):
+    u1 = 1 - (wa & 0x7fffff) 2^-23 in (0,1], u2 = (wb & 0x7fffff) 2^-23 in [0,1);
+    r = sqrt(-2 ln u1), (r cos 2pi u2, r sin 2pi u2)."""
+    u1 = 1.0 - (np.asarray(wa, np.uint32) & np.uint32(0x7FFFFF)).astype(np.float64) * TWO_M23
+    u2 = (np.asarray(wb, np.uint32) & np.uint32(0x7FFFFF)).astype(np.float64) * TWO_M23
     r = np.sqrt(-2.0 * np.log(u1))
     ang = 2.0 * np.pi * u2
     return r * np.cos(ang), r * np.sin(ang)

@@ -252,15 +252,17 @@ def main():
     run_case("cha_mlp16_K1", "Cha", cha, "mlp", {"neurons": [16, 16]}, 4, 64, 1, 20250725, workdir=wd)
     run_case("cha_mlp16_K4", "Cha", cha, "mlp", {"neurons": [16, 16]}, 4, 64, 4, 7, epoch=3, point_base=100, workdir=wd)
     run_case("cha_mlp128x4_K20", "Cha", cha, "mlp", {"neurons": [128] * 4}, 3, 64, 20, 20250725, workdir=wd)
-    run_case("cha_zero_K2", "Cha", cha, "mlp", {"neurons": [8]}, 3, 32, 2, 11, workdir=wd, zero=True)
+    run_case("cha_zero_K2", "Cha", cha, "mlp", {"neurons": [8]}, 3, 64, 2, 11, workdir=wd, zero=True)
+    run_case("cha_mlp64x3_K50", "Cha", cha, "mlp", {"neurons": [64] * 3}, 2, 128, 50, 1, epoch=7, workdir=wd)
     # HJB: OU + GMM, PISGradNet (reduced width), zero net (iteration 1)
-    run_case("ou_pis32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 3, 32, 2, 2, workdir=wd)
-    run_case("ou_mlp16_K2", "OUProcessEquation", ou, "mlp", {"neurons": [16, 16]}, 3, 32, 2, 5, workdir=wd)
-    run_case("ou_zero_K1", "OUProcessEquation", ou, "mlp", {"neurons": [8]}, 3, 32, 1, 2, workdir=wd, zero=True)
+    run_case("ou_pis32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 3, 64, 2, 2, workdir=wd)
+    run_case("ou_mlp16_K2", "OUProcessEquation", ou, "mlp", {"neurons": [16, 16]}, 3, 64, 2, 5, workdir=wd)
+    run_case("ou_mlp128x4_K3", "OUProcessEquation", ou, "mlp", {"neurons": [128] * 4}, 2, 64, 3, 9, workdir=wd)
+    run_case("ou_zero_K1", "OUProcessEquation", ou, "mlp", {"neurons": [8]}, 3, 64, 1, 2, workdir=wd, zero=True)
     # Fully-nonlinear case_1 (GBM): SDGD v=100 and full-Hessian (v=0), MLP 3x16
-    run_case("gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 3, 32, 2, 3,
+    run_case("gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 3, 64, 2, 3,
              v=100, workdir=wd)
-    run_case("gbm_mlp16_full_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 16, 1, 4,
+    run_case("gbm_mlp16_full_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 64, 1, 4,
              workdir=wd)
     shutil.rmtree(wd)
 

@@ -1,0 +1,61 @@
+"""The C-ABI library builds, loads on a host without a GPU, and exports exactly the symbols
+include/dpi.h declares; the ctypes mirror's constants equal the header's."""
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "dpi.h"
+
+
+def _header_functions():
+    txt = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return set(re.findall(r"^\s*(?:int|size_t)\s+(dpi_\w+)\s*\(", txt, flags=re.M))
+
+
+def _header_defines():
+    return {k: int(v.strip("()")) for k, v in re.findall(r"#define\s+(DPI_\w+)\s+(\(?-?\d+\)?)", HEADER.read_text())}
+
+
+def test_header_and_ctypes_agree():
+    from deeppicarditeration_amd import _lib
+    assert _header_functions() == set(_lib.SIGNATURES)
+    for k, v in _header_defines().items():
+        assert getattr(_lib, k) == v, k
+
+
+def test_library_loads_and_exports_every_symbol():
+    from deeppicarditeration_amd import _lib
+    from deeppicarditeration_amd.build import OUT, build
+    build()
+    lib = _lib.load()
+    assert lib.dpi_abi_version() == _lib.DPI_ABI_VERSION
+    out = subprocess.run(["nm", "-D", "--defined-only", str(OUT)], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (dpi_\w+)", out))
+    assert _header_functions() <= exported
+
+
+def test_host_side_argument_errors_without_gpu():
+    import ctypes
+    from deeppicarditeration_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    assert lib.dpi_problem_create_cha(0, 1.0, 5.0, 1.0, h) == _lib.DPI_ERR_ARG
+    assert "cha" in _lib.last_error()
+    assert lib.dpi_problem_create_cha(100, 1.0, 5.0, 1.0, h) == 0
+    n = ctypes.c_void_p()
+    assert lib.dpi_net_create_zero(n) == 0
+    assert lib.dpi_workspace_bytes(h, n, 16, 4096) > 0
+    # label call argument validation happens before any device work
+    rc = lib.dpi_label_moments(h, n, ctypes.c_void_p(16), 4, 4096, 50, 1, 0, 0, 0, 100, 3, ctypes.c_void_p(16),
+                               ctypes.c_void_p(16), 1 << 30, None)
+    assert rc == _lib.DPI_ERR_ARG and "multiple of 64" in _lib.last_error()
+    assert lib.dpi_net_destroy(n) == 0 and lib.dpi_problem_destroy(h) == 0
+
+
+def test_product_fails_loudly_without_library(tmp_path, monkeypatch):
+    from deeppicarditeration_amd import _lib
+    with pytest.raises(_lib.DPIError):
+        _lib.load(tmp_path / "missing.so")

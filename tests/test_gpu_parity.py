@@ -1,0 +1,159 @@
+"""GPU parity of the HIP label path (libdpi_hip.so via the C-ABI) against
+(a) the reference's own outputs (golden fixtures, fp64 reference with injected Philox noise) and
+(b) the CPU oracle (fp64 numpy restatement) on the same seeded inputs.
+
+Tolerance (north star): rel-L2 <= 1e-4 of the fp32 HIP labels vs the fp64 reference, measured
+separately on the value column and the gradient block.  Expected ~1e-7 (fp32 rounding).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    import deeppicarditeration_amd._lib as L
+    L.load()  # fail loudly if the HIP library is missing
+
+
+from golden_util import CASES, load, oracle_equation, oracle_net  # noqa: E402
+from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
+from oracle import dpi_oracle as O  # noqa: E402
+
+SUPPORTED = [c for c in CASES if not (c.startswith("gbm") or "_pis" in c)]
+
+
+@pytest.mark.parametrize("case", SUPPORTED)
+def test_golden_reference_parity(case):
+    f = load(case)
+    eq = product_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    y = gen.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu().numpy()
+    parts = rel_l2_parts(y, f["y"])
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2"])
+def test_sample_points_match_oracle(case):
+    f = load(case)
+    eq = product_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    n = 257
+    tx, _ = gen.sample_t_and_x(n, point_base=int(f["point_base"]))
+    ref = O.sample_points(oracle_equation(f), n, int(f["seed"]), int(f["epoch"]), int(f["point_base"]))
+    tx = tx.cpu().double().numpy()
+    np.testing.assert_allclose(tx[:, 0], ref[:, 0], rtol=2e-7, atol=1e-7)
+    np.testing.assert_allclose(tx[:, 1:], ref[:, 1:], rtol=0, atol=2e-5)
+    # the golden fixture's points came from the same contract
+    np.testing.assert_allclose(tx[: int(f["n"])], f["tx"], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2"])
+def test_terminal_and_integral_estimators(case):
+    f = load(case)
+    eq = product_equation(f)
+    net = product_module(f, eq)
+    oeq = oracle_equation(f)
+    onet = oracle_net(f, oeq)
+    gen = generator(f, eq, net)
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    pb = int(f["point_base"])
+    yT = gen.estimate_terminal_with_gradients(tx, point_base=pb).cpu().numpy()
+    yI = gen.estimate_integral_with_gradients(tx, point_base=pb).cpu().numpy()
+    _, rT, rI = O.labels_grad(oeq, onet, f["tx"], int(f["M"]), int(f["K"]), int(f["seed"]), int(f["epoch"]), pb,
+                              return_parts=True)
+    pT, pI = rel_l2_parts(yT, rT), rel_l2_parts(yI, rI)
+    assert pT["value"] < TOL and pT["grad"] < TOL, pT
+    assert pI["value"] < TOL and pI["grad"] < TOL, pI
+
+
+def _random_mlp(eq, widths, seed):
+    import deeppicarditeration_amd as dpi
+    torch.manual_seed(seed)
+    return dpi.construct_mlp(1 + eq.nx, 1, widths, ["ELU"] * len(widths), None)
+
+
+def _oracle_mlp(m):
+    lin = [l for l in m if isinstance(l, torch.nn.Linear)]
+    return O.MLP([l.weight.detach().double().numpy() for l in lin], [l.bias.detach().double().numpy() for l in lin],
+                 ["ELU"] * (len(lin) - 1))
+
+
+def test_burgers_full_network_K50_vs_oracle():
+    """Config-2 network (4x128 ELU) and K = 50 at a size the fp64 oracle finishes quickly."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    net = _random_mlp(eq, [128] * 4, 3)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=512,
+                                  n_estimate_integral=512, n_euler_steps=50, seed=1, epoch=0)
+    tx, y = gen.sample_with_gradients(3)
+    oeq = O.Cha(100, 1.0, 5.0, 1.0)
+    ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 512, 50, 1, 0, 0)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_hjb_ou_mlp_vs_oracle():
+    import deeppicarditeration_amd as dpi
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    net = _random_mlp(eq, [64] * 3, 4)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                  n_estimate_integral=256, n_euler_steps=10, seed=2, epoch=5)
+    tx, y = gen.sample_with_gradients(3)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 256, 10, 2, 5, 0)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_full_size_determinism_and_shard_invariance():
+    """BASELINE config 2 size (16 x 4096 paths, K = 50): bitwise-reproducible labels, and moments
+    computed as two MC shards + dpi_moments_reduce equal the single call bit for bit."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    net = _random_mlp(eq, [128] * 4, 5)
+    M = 4096
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=50, seed=1)
+    tx, _ = gen.sample_t_and_x(16, point_base=0)
+    ws = gen.point_baseline(tx)
+    full = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+    again = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+    assert torch.equal(full, again)
+    for G in (2, 4, 8):
+        parts = torch.stack([gen.label_moments(tx, 0, M, r * M // G, (r + 1) * M // G, L.DPI_BOTH, ws)
+                             for r in range(G)]).contiguous()
+        out = torch.empty_like(full)
+        L.check(gen.lib.dpi_moments_reduce(L.c_void_p(parts.data_ptr()), G, 16, 100, L.c_void_p(out.data_ptr()),
+                                           L.c_void_p(torch.cuda.current_stream().cuda_stream)), "moments_reduce")
+        assert torch.equal(out, full), G
+    y = gen.finalize(full, M, L.DPI_BOTH, ws)
+    assert torch.isfinite(y).all()
+    # linearity: terminal + integral estimators == joint estimator (to fp32 rounding)
+    yT = gen.finalize(gen.label_moments(tx, 0, M, 0, M, L.DPI_TERMINAL, ws), M, L.DPI_TERMINAL, ws)
+    yI = gen.finalize(gen.label_moments(tx, 0, M, 0, M, L.DPI_INTEGRAL, ws), M, L.DPI_INTEGRAL, ws)
+    torch.testing.assert_close(yT + yI, y, rtol=1e-5, atol=1e-5)
+
+
+def test_unsupported_configurations_fail_loudly():
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd._lib import DPIError
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    with pytest.raises(NotImplementedError):
+        dpi.OnlineDataGenerator(eq, dpi.construct_mlp(101, 1, [16], ["Tanh"], None), 1, 1, device="cuda:0",
+                                t_always_uniform=True, n_estimate_terminal=64, n_estimate_integral=64)
+    with pytest.raises(ValueError):
+        dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(), 1, 1, device="cuda:0", t_always_uniform=True,
+                                n_estimate_terminal=100, n_estimate_integral=100)
+    with pytest.raises(DPIError):
+        dpi.construct_mlp  # noqa: B018
+        dpi.GBMEquationComplexExact(100).dpi_problem()
