@@ -31,9 +31,10 @@ class ShardedLabeler:
         if self.world == 1:
             return mom
         import torch.distributed as dist
-        parts = torch.empty((self.world,) + tuple(mom.shape), dtype=mom.dtype, device=mom.device)
-        dist.all_gather_into_tensor(parts, mom.contiguous(), group=self.group)
-        return self.gen.moments_reduce(parts)
+        mom = mom.contiguous()
+        flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
+        dist.all_gather_into_tensor(flat, mom, group=self.group)  # rank-major concatenation
+        return self.gen.moments_reduce(flat.view((self.world,) + tuple(mom.shape)))
 
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""

@@ -401,3 +401,39 @@ def rel_l2(a, b):
 
 def rel_l2_parts(a, b):
     return {"value": rel_l2(a[:, :1], b[:, :1]), "grad": rel_l2(a[:, 1:], b[:, 1:]), "all": rel_l2(a, b)}
+
+
+# ----------------------------------------------------------------------------- moments (sharding)
+def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0):
+    """Per-path contribution rows c (len(m), 1+nx) whose mean (+ g(x) in column 0) is the label
+    (picard/data.py:923-925, :523-526), for one point and MC indices m."""
+    t = float(tx_row[0])
+    x = np.asarray(tx_row[1:], np.float64)[None]
+    T, a = eq.T, eq.alpha_sqrt
+    g_x = eq.g(x)[0, 0]
+    fb = _f_and_extras(eq, net, np.array([[t]]), x)[0][0, 0]
+    S_T, S_s, U, _ = path_noise(eq, ig, np.asarray(m), K, seed, epoch)
+    W_T = math.sqrt((T - t) / K) * S_T
+    Y = W_T / (T - t) / a
+    cT = eq.g(x + a * W_T) - g_x
+    s = (U * (T - t) + t)[:, None]
+    W_s = np.sqrt((s - t) / K) * S_s
+    f, _ = _f_and_extras(eq, net, s, x + a * W_s)
+    cI = (T - t) * (f - fb)
+    Ys = W_s / (s - t) / a
+    c = np.concatenate([cT + cI + fb * (T - t), cT * Y + cI * Ys], -1)
+    return c, g_x
+
+
+def tree_sum_f32(values):
+    """The device's canonical fixed-order sum (csrc/dpi_kernels.hip tree_sum): zero-pad to a
+    power of two >= 64 and add as a perfect binary tree in index order, in fp32.  values: (cnt, ...)."""
+    v = np.asarray(values, np.float32)
+    p2 = 64
+    while p2 < v.shape[0]:
+        p2 *= 2
+    pad = np.zeros((p2 - v.shape[0],) + v.shape[1:], np.float32)
+    v = np.concatenate([v, pad], 0)
+    while v.shape[0] > 1:
+        v = (v[0::2] + v[1::2]).astype(np.float32)
+    return v[0]

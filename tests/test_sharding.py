@@ -1,0 +1,99 @@
+"""Multi-rank label sharding (deeppicarditeration_amd/sharding.py) on CPU with the gloo backend:
+world_size 2 ranks split the MC indices, all-gather their moments and reduce them with the
+canonical tree; the labels must equal the single-rank result bit for bit.  The per-rank moment
+computation is the oracle (fp64 contributions -> fp32 64-path blocks -> canonical tree), standing
+in for dpi_label_moments, so this checks the sharding logic and collective, not the kernel."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import dpi_oracle as O
+
+NX, M, K, N = 100, 512, 3, 3
+
+
+def _problem():
+    rng = np.random.default_rng(0)
+    eq = O.Cha(NX, 1.0, 5.0, 1.0)
+    W = [rng.normal(0, 0.1, (16, NX + 1)), rng.normal(0, 0.25, (16, 16)), rng.normal(0, 0.25, (1, 16))]
+    b = [rng.normal(0, 0.1, 16), rng.normal(0, 0.1, 16), rng.normal(0, 0.1, 1)]
+    net = O.MLP(W, b, ["ELU", "ELU"])
+    tx = O.sample_points(eq, N, seed=7)
+    return eq, net, tx
+
+
+class OracleGen:
+    """Stands in for OnlineDataGenerator's moment building blocks (same method names)."""
+
+    def __init__(self, eq, net):
+        self.eq, self.net = eq, net
+        self.n_estimate_terminal = self.n_estimate_integral = M
+        self.gx = None
+
+    def point_baseline(self, tx):
+        return tx
+
+    def label_moments(self, tx, point_base, M_, m0, m1, flags, ws):
+        out = np.zeros((tx.shape[0], 2, NX + 1), np.float32)
+        gx = []
+        for r in range(tx.shape[0]):
+            c, g = O.path_contributions(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), K, 7)
+            gx.append(g)
+            blocks = c.reshape(-1, 64, NX + 1)
+            s1 = np.stack([O.tree_sum_f32(bk.astype(np.float32)) for bk in blocks])  # per-block sums
+            s2 = np.stack([O.tree_sum_f32((bk.astype(np.float32)) ** 2) for bk in blocks])
+            out[r, 0] = O.tree_sum_f32(s1)
+            out[r, 1] = O.tree_sum_f32(s2)
+        self.gx = np.array(gx)
+        return torch.from_numpy(out)
+
+    def moments_reduce(self, parts):
+        return torch.from_numpy(O.tree_sum_f32(parts.numpy()))
+
+    def finalize(self, mom, M_, flags, ws):
+        y = mom[:, 0].numpy() / M_
+        y[:, 0] += self.gx
+        return torch.from_numpy(y)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    lab = ShardedLabeler(OracleGen(eq, net), rank=rank, world=world)
+    y = lab.labels(tx, 0)
+    q.put((rank, y.numpy()))
+    dist.destroy_process_group()
+
+
+def test_shard_ranges():
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    assert [ShardedLabeler(None, r, 4).shard(4096) for r in range(4)] == [(0, 1024), (1024, 2048), (2048, 3072),
+                                                                           (3072, 4096)]
+    with pytest.raises(ValueError):
+        ShardedLabeler(None, 0, 3).shard(4096)
+
+
+def test_two_rank_gloo_labels_equal_single_rank():
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    single = ShardedLabeler(OracleGen(eq, net), 0, 1).labels(tx, 0).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29000 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0].tobytes() == res[1].tobytes()
+    assert res[0].tobytes() == single.tobytes()
+    # and the labels are the oracle's labels (to fp32 summation error)
+    ref = O.labels_grad(eq, net, tx, M, K, 7)
+    assert O.rel_l2(single, ref) < 1e-5
