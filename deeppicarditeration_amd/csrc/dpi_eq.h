@@ -26,8 +26,13 @@ struct EqDev {
   const float* logc;  // (ncomp) log pi_k - 0.5 (nx log 2pi + log det_k)   (utils.py:862-876)
   // GBMEquationComplexExact (equations.py:388-486)
   int nodes;
-  const float* gw;  // (nodes, 1+nx)
-  const float* gv;  // (nodes)
+  const float* gw;   // (nodes, 1+nx)
+  const float* gv;   // (nodes)
+  const float* gwsq; // (nodes) sum_d w_{k,1+d}^2
+  const float* gwv2; // (nodes, nx) v_k w_{k,1+d}^2   (diag of the exact Hessian, :444-449)
+  // Hessian approximation (DATA.HESSIAN_APPROXIMATION): sdgd_v > 0 = SDGD with v indices
+  // drawn with replacement (data.py:497-502), 0 = exact diagonal (data.py:1262-1272)
+  int sdgd_v;
 };
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
@@ -88,6 +93,54 @@ struct Eq<DPI_EQ_OU> {
     return e.ou_theta * A - 0.5f * e.alpha * B;
   }
   __device__ static __forceinline__ float ffc(const EqDev& e) { return -e.ou_d * e.ou_theta; }
+};
+
+// ------------------------------------------------------------------------------ GBM (fully nonlinear)
+template <>
+struct Eq<DPI_EQ_GBM> {
+  static constexpr int GRAD_FULL = 0;
+  // g(X) = sum_k v_k sin(w_k0 T + sum_d w_{k,1+d} X_d)   (equations.py:422-430)
+  __device__ static __forceinline__ void gstat(const EqDev& e, int d, float X, float* st) {
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      if (c < e.nodes) st[c] = fmaf(e.gw[c * (1 + e.nx) + 1 + d], X, st[c]);
+  }
+  __device__ static __forceinline__ float gfin(const EqDev& e, const float* st) {
+    float g = 0.f;
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      if (c < e.nodes) g = fmaf(e.gv[c], __sinf(fmaf(e.gw[c * (1 + e.nx)], e.T, st[c])), g);
+    return g;
+  }
+  __device__ static __forceinline__ void gacc(const EqDev& e, int d, float X, float z, float& A, float& B) {}
+  __device__ static __forceinline__ float ffv(const EqDev& e, float u, float gsum, float A, float B) { return 0.f; }
+  __device__ static __forceinline__ float ffc(const EqDev& e) { return 0.f; }
+  // exact-solution part of ffi at (s, X) given arg_k = w_k . [s, X]: -u*_t - 1/2 lap u* (:457-466);
+  // the -1/4 sum_d |H*_dd| part needs a pass over d (see gbm_abs_hess_partial).
+  __device__ static __forceinline__ float exact_scalar_terms(const EqDev& e, const float* arg) {
+    float r = 0.f;
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      if (c < e.nodes) {
+        const float sn = __sinf(arg[c]), cs = __cosf(arg[c]);
+        r -= e.gv[c] * e.gw[c * (1 + e.nx)] * cs;    // -u*_t
+        r += 0.5f * e.gv[c] * e.gwsq[c] * sn;        // -1/2 lap u* = +1/2 sum v |w|^2 sin
+      }
+    }
+    return r;
+  }
+  // sum over d in [d0, d1) step ds of |H*_dd| = |sum_k v_k w_kd^2 sin(arg_k)|
+  __device__ static __forceinline__ float abs_hess_partial(const EqDev& e, const float* sn, int d0, int ds) {
+    float r = 0.f;
+    for (int d = d0; d < e.nx; d += ds) {
+      float h = 0.f;
+#pragma unroll
+      for (int c = 0; c < NSG; ++c)
+        if (c < e.nodes) h = fmaf(e.gwv2[c * e.nx + d], sn[c], h);
+      r += fabsf(h);
+    }
+    return r;
+  }
 };
 
 }  // namespace dpi

@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -105,8 +106,8 @@ struct Lds {
 // cmul, vec[0:H] = base0 (layer-1 bias incl. W1x x), vec[H:2H] = w1t, vec[2H:3H] = wout,
 // vec[3H:4H] = c1, bh[l*H:(l+1)*H] = biases of hidden layers l >= 1.
 // If bx_out != nullptr (baseline mode) writes b1 + W1x S (per path) to bx_out[pp*bstride + h].
-template <int KIND, int H, int L>
-__device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, Lds& sh, int nxt, float& u_out,
+template <int KIND, int H, int L, class SH>
+__device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& sh, int nxt, float& u_out,
                                          float& gsum_out, float& gA_out, float& gB_out, float* bx_out,
                                          int bstride, int n_valid_paths) {
   constexpr int HT = H / 16;
@@ -268,6 +269,153 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, Lds&
   }
 }
 
+// LDS of the fully-nonlinear (GBM) path kernel: every weight matrix stays resident for the
+// 100-direction tangent sweep.  H <= 64, L <= 4.
+template <int H>
+struct LdsGbm {
+  static constexpr int WXS = NXP_MAX + 8;  // W1x row stride (WXS/4 = 2 mod 4)
+  static constexpr int WHS = H + 8;        // hidden row stride
+  float S[NXP_MAX * SS];
+  float W1x[H * WXS];
+  float Wh[3][H * WHS];
+  float vec[4 * HMAX];
+  float bh[4 * HMAX];
+  float xsh[NXP_MAX];
+  float hb[NXP_MAX];
+  float gst[4 * P * NSG];
+  float fst[4 * P * NSG];
+  float wx[NSG];
+  float tau[P], cmul[P], bsh[P], fbp[P];
+  unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
+};
+
+__device__ __forceinline__ float d2elu_from_a(float a) { return a > 0.f ? 0.f : a + 1.0f; }
+
+// Diagonal of the x-Hessian of u at (s, X_s) for this wave's 16 paths, contracted with the
+// path's SDGD index histogram: s1 = sum_d cnt[d] u_dd, s2 = sum_d cnt[d] |u_dd|.
+// Uses u_dd = sum_l < lam_l, elu''(z_l) * zdot_l^2 >, with lam_l = du/da_l (one backward pass)
+// and zdot_l = dz_l/dx_d (first-order tangents only): half the MACs of second-order
+// forward mode.  All GEMMs are v_mfma_f32_16x16x4_f32 in the hidden x path orientation.
+template <int H, int L>
+__device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt, float& s1_out,
+                                          float& s2_out) {
+  constexpr int HT = H / 16;
+  constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  float act[L][HT][4];
+  float lam[L][HT][4];
+  // forward
+#pragma unroll
+  for (int T = 0; T < HT; ++T) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    for (int t = 0; t < nxt; ++t) {
+      const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+      const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+      acc = mfma4(a.x, bc[0], acc);
+      acc = mfma4(a.y, bc[SS], acc);
+      acc = mfma4(a.z, bc[2 * SS], acc);
+      acc = mfma4(a.w, bc[3 * SS], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = sh.Wh[l - 1] + (16 * T + jj) * WHS + 4 * qq;
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+        acc = mfma4(a.x, act[l - 1][t][0], acc);
+        acc = mfma4(a.y, act[l - 1][t][1], acc);
+        acc = mfma4(a.z, act[l - 1][t][2], acc);
+        acc = mfma4(a.w, act[l - 1][t][3], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+    }
+  }
+  // adjoints lam_l = du/da_l
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lam[L - 1][T][r] = sh.vec[2 * H + 16 * T + 4 * qq + r];
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+    float Bm[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l + 1][t][r]) * lam[l + 1][t][r];
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)  // A[i][k] = W_{l+1}[k][i]: column 16T+jj, row 16t+4qq+r
+          acc = mfma4(sh.Wh[l][(16 * t + 4 * qq + r) * WHS + 16 * T + jj], Bm[t][r], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lam[l][T][r] = acc[r];
+    }
+  }
+  // tangent sweep over the state dimensions
+  float s1 = 0.f, s2 = 0.f;
+  for (int d = 0; d < e.nx; ++d) {
+    float z[HT][4];
+    float term = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+        term = fmaf(lam[0][T][r] * d2elu_from_a(act[0][T][r]), z[T][r] * z[T][r], term);
+      }
+#pragma unroll
+    for (int l = 1; l < L; ++l) {
+      float Bm[HT][4];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l - 1][t][r]) * z[t][r];
+#pragma unroll
+      for (int T = 0; T < HT; ++T) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* wrow = sh.Wh[l - 1] + (16 * T + jj) * WHS + 4 * qq;
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+          acc = mfma4(a.x, Bm[t][0], acc);
+          acc = mfma4(a.y, Bm[t][1], acc);
+          acc = mfma4(a.z, Bm[t][2], acc);
+          acc = mfma4(a.w, Bm[t][3], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          z[T][r] = acc[r];
+          term = fmaf(lam[l][T][r] * d2elu_from_a(act[l][T][r]), acc[r] * acc[r], term);
+        }
+      }
+    }
+    const float ud = qsum(term);
+    const float c = (float)sh.cnt[d * P + pp];
+    s1 = fmaf(c, ud, s1);
+    s2 = fmaf(c, fabsf(ud), s2);
+  }
+  s1_out = s1;
+  s2_out = s2;
+}
+
 // ------------------------------------------------------------------------------ kernels
 // Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
 template <int KIND>
@@ -317,7 +465,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 template <int KIND, bool ZERO>
 __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
                                                   float* __restrict__ gx, float* __restrict__ fb,
-                                                  float* __restrict__ bx) {
+                                                  float* __restrict__ bx, float* __restrict__ hb) {
   __shared__ float xs[NXP_MAX];
   __shared__ float act[4][HMAX];
   __shared__ float dbuf[2][HMAX];
@@ -337,6 +485,27 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
 #pragma unroll
     for (int c = 0; c < NSG; ++c) st[c] = block_sum(st[c], red);
     if (tid == 0) gx[i] = Eq<KIND>::gfin(e, st);
+  }
+  float Cb = 0.f;
+  if constexpr (KIND == DPI_EQ_GBM) {
+    // exact-solution part of ffi at (t, x) (equations.py:457-466)
+    float arg[NSG], sn[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      float v = 0.f;
+      if (c < e.nodes)
+        for (int d = tid; d < nx; d += NTH) v = fmaf(e.gw[c * F + 1 + d], xs[d], v);
+      v = block_sum(v, red);
+      arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, v) : 0.f;
+      sn[c] = __sinf(arg[c]);
+    }
+    const float ah = block_sum(Eq<KIND>::abs_hess_partial(e, sn, tid, NTH), red);
+    Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+    if (ZERO) {
+      for (int d = tid; d < NXP_MAX; d += NTH) hb[(size_t)i * NXP_MAX + d] = 0.f;
+      if (tid == 0) fb[i] = Cb;
+      return;
+    }
   }
   if (ZERO) {
     if (tid == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, 0.f, 0.f);
@@ -359,6 +528,45 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
       act[l][tid] = elu(acc);
     }
     __syncthreads();
+  }
+  if constexpr (KIND == DPI_EQ_GBM) {
+    // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
+    // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
+    __shared__ float lamb[4][HMAX];
+    __shared__ float ztb[2][64][NXP_MAX];
+    if (tid < H) lamb[L - 1][tid] = net.wout[tid];
+    __syncthreads();
+    for (int l = L - 2; l >= 0; --l) {
+      if (tid < H) {
+        const float* w = net.W[l + 1];
+        float acc = 0.f;
+        for (int h = 0; h < H; ++h) acc = fmaf(w[(size_t)h * H + tid], delu_from_a(act[l + 1][h]) * lamb[l + 1][h], acc);
+        lamb[l][tid] = acc;
+      }
+      __syncthreads();
+    }
+    for (int d = tid; d < nx; d += NTH) {
+      float ud = 0.f;
+      for (int h = 0; h < H; ++h) {
+        const float z = net.W1x[(size_t)h * nxp + d];
+        ztb[0][h][d] = z;
+        ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
+      }
+      int cz = 0;
+      for (int l = 1; l < L; ++l) {
+        const float* w = net.W[l];
+        for (int h = 0; h < H; ++h) {
+          float z = 0.f;
+          for (int k = 0; k < H; ++k) z = fmaf(w[(size_t)h * H + k], delu_from_a(act[l - 1][k]) * ztb[cz][k][d], z);
+          ztb[cz ^ 1][h][d] = z;
+          ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z * z, ud);
+        }
+        cz ^= 1;
+      }
+      hb[(size_t)i * NXP_MAX + d] = ud;
+    }
+    if (tid == 0) fb[i] = Cb;
+    return;
   }
   const float u = block_sum(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
   int cur = 0;
@@ -395,15 +603,18 @@ struct PathArgs {
   const float* gx;
   const float* fb;
   const float* bx;
+  const float* hb;  // GBM: baseline Hessian diagonal [n][NXP_MAX]
   float* partial;
   int n, nbp, m_begin, K, flags;
-  uint32_t k0, k1, c3t, c3s, c3i, point_base;
+  uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
 };
 
 // One workgroup = (point i, 64 consecutive MC indices).  See the file header.
 template <int KIND, int H, int L, bool ZERO>
 __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
-  __shared__ Lds sh;
+  constexpr bool GBM = KIND == DPI_EQ_GBM;
+  using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
+  __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = blockIdx.x / a.nbp, blk = blockIdx.x - i * a.nbp;
   const uint32_t ig = a.point_base + (uint32_t)i;
@@ -433,6 +644,32 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
     for (int l = 1; l < L; ++l)
       for (int h = tid; h < H; h += NTH) sh.bh[l * H + h] = net.b[l][h];
   }
+  if constexpr (GBM) {
+    if (!ZERO) {  // all weights resident for the tangent sweep
+      constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+      for (int idx = tid; idx < H * nxp; idx += NTH) {
+        const int h = idx / nxp, d = idx - h * nxp;
+        sh.W1x[h * WXS + d] = net.W1x[idx];
+      }
+      for (int l = 1; l < L; ++l)
+        for (int idx = tid; idx < H * H; idx += NTH) {
+          const int h = idx / H, k = idx - h * H;
+          sh.Wh[l - 1][h * WHS + k] = net.W[l][idx];
+        }
+    }
+    for (int d = tid; d < nxp; d += NTH) sh.hb[d] = d < nx ? a.hb[(size_t)i * NXP_MAX + d] : 0.f;
+    for (int idx = tid; idx < nxp * P / 4; idx += NTH) reinterpret_cast<uint32_t*>(sh.cnt)[idx] = 0u;
+    if (wv == 0) {  // w_k . x for this point
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float v = 0.f;
+        if (c < e.nodes)
+          for (int d = lane; d < nx; d += 64) v = fmaf(e.gw[c * F + 1 + d], txr[1 + d], v);
+        v = wave_sum(v);
+        if (lane == 0) sh.wx[c] = v;
+      }
+    }
+  }
   // s ~ U(t, T] for this lane's path (data.py:359); integral/terminal step multipliers
   const float U = u01_oc(philox4x32_10(0u, m, ig, a.c3s, a.k0, a.k1).x);
   const float s = fmaf(U, tmt, t);
@@ -449,9 +686,28 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
 
   // ---------------- phase 1: K-step Euler–Maruyama rollouts
   float ST[8][4];
-  float gst[NSG];
+  float gst[NSG], fst[NSG];
 #pragma unroll
-  for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
+  for (int c = 0; c < NSG; ++c) gst[c] = fst[c] = 0.f;
+  if constexpr (GBM) {
+    // SDGD indices (data.py:497-502): v draws in [0, nx) with replacement -> histogram cnt[d][path]
+    if (INTG && wv == 1) {  // one wave owns the histogram (wave 1 has 12 rollout blocks, not 13)
+      if (e.sdgd_v > 0) {
+        for (int q0 = 0; q0 < e.sdgd_v; q0 += 4) {
+          const u32x4 w = philox4x32_10((uint32_t)(q0 >> 2), m, ig, a.c3q, a.k0, a.k1);
+          const uint32_t ws4[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (q0 + r < e.sdgd_v) {
+              const int idx = (int)(((uint64_t)ws4[r] * (uint32_t)nx) >> 32);
+              sh.cnt[idx * P + lane] += 1;
+            }
+        }
+      } else {
+        for (int d = 0; d < nx; ++d) sh.cnt[d * P + lane] = 1;  // exact diagonal: every d once
+      }
+    }
+  }
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     const int j = wv + 4 * c;  // terminal dim-blocks of this wave
@@ -495,11 +751,22 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
       for (int q = 0; q < 4; ++q) {
         const int d = 4 * j + q;
         sh.S[d * SS + lane] = d < nx ? sv[q] : 0.f;
+        if constexpr (GBM) {  // w_k . S for the exact-solution terms at X_s = x + cI S
+          if (d < nx) {
+#pragma unroll
+            for (int c = 0; c < NSG; ++c)
+              if (c < e.nodes) fst[c] = fmaf(e.gw[c * F + 1 + d], sv[q], fst[c]);
+          }
+        }
       }
     }
   }
 #pragma unroll
   for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = gst[c];
+  if constexpr (GBM) {
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fst[c];
+  }
   __syncthreads();
   float gT = 0.f;
   if (TERM) {
@@ -511,12 +778,47 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   }
   const float ap = TERM ? gT - g_x : 0.f;  // (g(X_T) - g(x)) (data.py:923)
 
-  // ---------------- phase 2: u, grad u at (s, X_s) and f
-  float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
-  if (!ZERO && INTG) mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
-  {
+  // ---------------- phase 2: u, grad u (or the SDGD Hessian diagonal) at (s, X_s) and f
+  if constexpr (!GBM) {
+    float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
+    if (!ZERO && INTG) mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
     const int pp = 16 * wv + (lane & 15);
     if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
+  } else {
+    // ffi (equations.py:457-466) with u_ii from SDGD (data.py:1273-1303); the baseline f_b
+    // gathers the point's Hessian diagonal at this path's indices (data.py:1293-1302).
+    const int jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
+    float s1 = 0.f, s2 = 0.f;
+    if (!ZERO && INTG) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+    const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
+    const float c1 = 0.5f * (1.0f - e.alpha) * (float)nx / vv, c2 = 0.25f * (float)nx / vv;
+    float arg[NSG], sn[NSG];
+    const float spp = sh.tau[pp], cpp = sh.cmul[pp];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      arg[c] = 0.f;
+      if (c < e.nodes) {
+        const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
+                          sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
+        arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+      }
+      sn[c] = __sinf(arg[c]);
+    }
+    const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
+    float b1 = 0.f, b2 = 0.f;  // baseline Hessian diagonal gathered at this path's indices
+    for (int d = qq; d < nx; d += 4) {
+      const float c = (float)sh.cnt[d * P + pp], h = sh.hb[d];
+      b1 = fmaf(c, h, b1);
+      b2 = fmaf(c, fabsf(h), b2);
+    }
+    b1 = qsum(b1);
+    b2 = qsum(b2);
+    const float f = c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+    const float fbp = f_b + c1 * b1 + c2 * b2;
+    if (qq == 0) {
+      sh.bsh[pp] = INTG ? tmt * (f - fbp) : 0.f;
+      sh.fbp[pp] = fbp;
+    }
   }
   __syncthreads();
 
@@ -526,7 +828,12 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   float* out = a.partial + (size_t)i * 2 * F * a.nbp + blk;
   const int nbs = a.nbp;
   if (wv == 0) {
-    const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
+    float fbt;
+    if constexpr (GBM)
+      fbt = sh.fbp[lane];
+    else
+      fbt = f_b + Eq<KIND>::ffc(e);
+    const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
     const float s1 = wave_sum(c0), s2 = wave_sum(c0 * c0);
     if (lane == 0) {
       out[0] = s1;
@@ -673,6 +980,8 @@ int dpi_last_error(char* buf, size_t len) {
   return (int)g_err.size();
 }
 
+int dpi_problem_destroy(dpi_problem p);
+
 static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
   auto* p = new dpi_problem_s();
   std::memset(&p->e, 0, sizeof(p->e));
@@ -728,7 +1037,37 @@ int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double m
 
 int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
                            dpi_problem* out) {
-  return fail(DPI_ERR_UNSUPPORTED, "GBMEquationComplexExact: not yet supported by this build");
+  if (!out || nx < 1 || nx > NXP_MAX || n_nodes < 1 || n_nodes > NSG || !w || !v)
+    return fail(DPI_ERR_ARG, "gbm: bad arguments (1 <= n_nodes <= 8, nx <= 128)");
+  auto* p = new_problem(DPI_EQ_GBM, nx, alpha, T);
+  p->e.nodes = n_nodes;
+  const int F = 1 + nx;
+  std::vector<float> gw((size_t)n_nodes * F), gv(n_nodes), wsq(n_nodes), wv2((size_t)n_nodes * nx);
+  for (int c = 0; c < n_nodes; ++c) {
+    double sq = 0;
+    for (int d = 0; d < F; ++d) gw[(size_t)c * F + d] = (float)w[(size_t)c * F + d];
+    for (int d = 0; d < nx; ++d) {
+      const double wd = w[(size_t)c * F + 1 + d];
+      sq += wd * wd;
+      wv2[(size_t)c * nx + d] = (float)(v[c] * wd * wd);
+    }
+    gv[c] = (float)v[c];
+    wsq[c] = (float)sq;
+  }
+  int rc;
+  if ((rc = upload(p, gw, &p->e.gw)) || (rc = upload(p, gv, &p->e.gv)) || (rc = upload(p, wsq, &p->e.gwsq)) ||
+      (rc = upload(p, wv2, &p->e.gwv2))) {
+    dpi_problem_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return 0;
+}
+
+int dpi_problem_set_hessian_approximation(dpi_problem p, int sdgd_v) {
+  if (!p || sdgd_v < 0 || sdgd_v > 255) return fail(DPI_ERR_ARG, "hessian approximation: 0 <= v <= 255");
+  p->e.sdgd_v = sdgd_v;
+  return 0;
 }
 
 int dpi_problem_destroy(dpi_problem p) {
@@ -845,7 +1184,7 @@ int dpi_net_destroy(dpi_net net) {
 
 // Workspace: gx[n] | fb[n] | bx[n][H] | partial[n][nbp][2][F]   (256-B aligned pieces)
 struct WsLayout {
-  size_t gx, fb, bx, partial, total;
+  size_t gx, fb, bx, hb, partial, total;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
@@ -855,7 +1194,8 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   w.gx = 0;
   w.fb = al256((size_t)n * 4);
   w.bx = w.fb + al256((size_t)n * 4);
-  w.partial = w.bx + al256((size_t)n * H * 4);
+  w.hb = w.bx + al256((size_t)n * H * 4);
+  w.partial = w.hb + al256((size_t)n * NXP_MAX * 4);
   w.total = w.partial + (size_t)n * nbp * 2 * F * 4;
   return w;
 }
@@ -884,6 +1224,10 @@ extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t e
       hipLaunchKernelGGL(k_sample_points<DPI_EQ_OU>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
                          eps, p->alpha_init_sqrt, tx);
       break;
+    case DPI_EQ_GBM:
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_GBM>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
+                         eps, p->alpha_init_sqrt, tx);
+      break;
     default:
       return fail(DPI_ERR_UNSUPPORTED, "sample_points: equation kind");
   }
@@ -896,7 +1240,7 @@ struct Launch {
   bool baseline;
   const float* tx;
   int n;
-  float *gx, *fb, *bx;
+  float *gx, *fb, *bx, *hb;
   const PathArgs* a;
   int nblocks;
   hipStream_t st;
@@ -906,7 +1250,7 @@ template <int KIND, int H, int L, bool Z>
 static void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTH), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
-                       q.bx);
+                       q.bx, q.hb);
   else
     hipLaunchKernelGGL((k_paths<KIND, H, L, Z>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
 }
@@ -917,27 +1261,39 @@ static bool dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch&
     do_launch<KIND, 16, 1, true>(p, net, q);
     return true;
   }
+  const int H = net->d.H, L = net->d.L;
   if (q.baseline) {  // the baseline kernel is shape-generic
+    if (KIND == DPI_EQ_GBM && H > 64) return false;
     do_launch<KIND, 16, 1, false>(p, net, q);
     return true;
   }
-  const int H = net->d.H, L = net->d.L;
+  if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
 #define DPI_SHAPE(HH, LL)                      \
   if (H == HH && L == LL) {                    \
     do_launch<KIND, HH, LL, false>(p, net, q); \
     return true;                               \
   }
-  DPI_SHAPE(128, 4)
-  DPI_SHAPE(128, 3)
-  DPI_SHAPE(128, 2)
-  DPI_SHAPE(64, 3)
-  DPI_SHAPE(64, 2)
-  DPI_SHAPE(32, 2)
-  DPI_SHAPE(16, 1)
-  DPI_SHAPE(16, 2)
-  DPI_SHAPE(16, 3)
+    DPI_SHAPE(64, 3)
+    DPI_SHAPE(64, 2)
+    DPI_SHAPE(32, 2)
+    DPI_SHAPE(32, 3)
+    DPI_SHAPE(16, 1)
+    DPI_SHAPE(16, 2)
+    DPI_SHAPE(16, 3)
+    return false;
+  } else {
+    DPI_SHAPE(128, 4)
+    DPI_SHAPE(128, 3)
+    DPI_SHAPE(128, 2)
+    DPI_SHAPE(64, 3)
+    DPI_SHAPE(64, 2)
+    DPI_SHAPE(32, 2)
+    DPI_SHAPE(16, 1)
+    DPI_SHAPE(16, 2)
+    DPI_SHAPE(16, 3)
 #undef DPI_SHAPE
-  return false;
+    return false;
+  }
 }
 
 static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
@@ -946,6 +1302,8 @@ static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Lau
       return dispatch<DPI_EQ_CHA>(p, net, q);
     case DPI_EQ_OU:
       return dispatch<DPI_EQ_OU>(p, net, q);
+    case DPI_EQ_GBM:
+      return dispatch<DPI_EQ_GBM>(p, net, q);
     default:
       return false;
   }
@@ -968,7 +1326,8 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
   if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
-  Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), nullptr, 0, (hipStream_t)stream};
+  Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), nullptr, 0,
+           (hipStream_t)stream};
   if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "point_baseline: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
   return 0;
@@ -995,6 +1354,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.gx = (const float*)(b + w.gx);
   a.fb = (const float*)(b + w.fb);
   a.bx = (const float*)(b + w.bx);
+  a.hb = (const float*)(b + w.hb);
   a.partial = partial;
   a.n = n;
   a.nbp = nbp;
@@ -1006,9 +1366,10 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.c3t = DPI_TAG_TERM | (epoch << 8);
   a.c3s = DPI_TAG_S | (epoch << 8);
   a.c3i = DPI_TAG_INT | (epoch << 8);
+  a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.point_base = point_base;
   hipStream_t st = (hipStream_t)stream;
-  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, &a, n * nbp, st};
+  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
   if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,

@@ -33,6 +33,21 @@ def _stream(device):
     return _lib.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def _hessian_approximation(cfg):
+    """DATA.HESSIAN_APPROXIMATION ({method, kwargs: {v}}; config.py:99-101) -> (method, v)."""
+    if cfg is None:
+        return None, 0
+    get = (lambda k, d=None: cfg.get(k, d)) if isinstance(cfg, dict) else (lambda k, d=None: getattr(cfg, k, d))
+    method = get("method")
+    if method is None:
+        return None, 0
+    kw = get("kwargs") or {}
+    v = kw.get("v") if isinstance(kw, dict) else getattr(kw, "v", None)
+    if v is None or not (1 <= int(v) <= 255):
+        raise ValueError(f"SDGD needs 1 <= v <= 255 (got {v})")
+    return method, int(v)
+
+
 class OnlineDataGenerator:
     """picard/data.py:369-431 (constructor), :211-223 / :1208-1218 (label entry points)."""
 
@@ -51,9 +66,12 @@ class OnlineDataGenerator:
             raise NotImplementedError("t_always_uniform=False (product-of-uniforms t sampler) is not built yet")
         if estimate_delta_t and estimate_delta_t > 0:
             raise NotImplementedError("TD estimators (ESTIMATE_DELTA_T > 0) are out of scope for this build")
-        method = getattr(hessian_approximation, "method", None) if hessian_approximation is not None else None
-        if method is not None:
-            raise NotImplementedError(f"hessian approximation {method!r} is not built yet")
+        method, sdgd_v = _hessian_approximation(hessian_approximation)
+        if method is not None:  # data.py:115-123
+            if method not in equation.supported_approximate_methods:
+                raise AssertionError(f"Current equation does not support the method {method}")
+            if method != "SDGD":
+                raise NotImplementedError(f"hessian approximation {method!r}")
         self.equation = equation
         self.solution = solution
         self.N, self.i = N, i
@@ -83,6 +101,10 @@ class OnlineDataGenerator:
         solution.eval()
         self.net = DeviceNet.from_module(solution, 1 + equation.nx)
         self.problem = equation.dpi_problem()
+        if equation.has_hessian_term:
+            _lib.check(self.lib.dpi_problem_set_hessian_approximation(self.problem, sdgd_v),
+                       "dpi_problem_set_hessian_approximation")
+        self.sdgd_v = sdgd_v
         self._ws = None
 
     # ------------------------------------------------------------------ buffers

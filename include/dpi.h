@@ -12,6 +12,7 @@
  *   dpi_problem_create_cha   picard/equations.py:266-338  Cha(nx, alpha, k, T)
  *   dpi_problem_create_ou    picard/equations.py:489-714  OUProcessEquation(...) + utils.py:792-914 GMM
  *   dpi_problem_create_gbm   picard/equations.py:388-486  GBMEquationComplexExact(nx, alpha, T)
+ *   dpi_problem_set_hessian_approximation  picard/data.py:115-123, :497-502  HESSIAN_APPROXIMATION (SDGD v)
  *   dpi_net_create_zero      picard/solution.py:330-337   ZeroSolution (iteration 1)
  *   dpi_net_create_mlp       picard/solution.py:123-135   construct_mlp (state-dict order)
  *   dpi_sample_points        picard/data.py:161-167, :211-217  sample_t_always_uniform + equation.sample_x
@@ -83,13 +84,18 @@ int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double m
 /* w: (n_nodes, 1+nx); v: (n_nodes) */
 int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
                            dpi_problem* out);
+/* DATA.HESSIAN_APPROXIMATION for equations with a Hessian term (GBM): sdgd_v = 0 uses the exact
+ * Hessian diagonal (picard/data.py:1262-1272); 1 <= sdgd_v <= 255 draws v indices in [0, nx)
+ * with replacement per path (SDGD, data.py:497-502, 1273-1303). */
+int dpi_problem_set_hessian_approximation(dpi_problem p, int sdgd_v);
 int dpi_problem_destroy(dpi_problem p);
 
 /* --- networks u(t, x): weights uploaded once per Picard iteration into a library handle --- */
 int dpi_net_create_zero(dpi_net* out);
 /* params: host fp32, torch state-dict order of construct_mlp(n_in, 1, widths, act):
  *   W0 (widths[0] x n_in), b0, W1 (widths[1] x widths[0]), b1, ..., Wout (1 x widths[-1]), bout.
- * Supported (width, n_hidden): all hidden widths equal, one of 16/32/64/128, n_hidden 1..4. */
+ * Supported (width, n_hidden): all hidden widths equal, one of 16/32/64/128, n_hidden 1..4
+ * (GBM: width <= 64). */
 int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params,
                        size_t n_params, dpi_net* out);
 int dpi_net_destroy(dpi_net net);

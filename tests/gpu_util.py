@@ -38,9 +38,11 @@ def product_module(f, eq):
 
 def generator(f, eq, module, M=None, K=None):
     M = int(f["M"]) if M is None else M
+    v = int(f["v"])
+    hess = {"method": "SDGD", "kwargs": {"v": v}} if v > 0 else None
     return dpi.OnlineDataGenerator(eq, module, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
                                    n_estimate_integral=M, n_euler_steps=int(f["K"]) if K is None else K,
-                                   seed=int(f["seed"]), epoch=int(f["epoch"]))
+                                   seed=int(f["seed"]), epoch=int(f["epoch"]), hessian_approximation=hess)
 
 
 def rel_l2_parts(a, b):

@@ -26,7 +26,7 @@ from golden_util import CASES, load, oracle_equation, oracle_net  # noqa: E402
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
-SUPPORTED = [c for c in CASES if not (c.startswith("gbm") or "_pis" in c)]
+SUPPORTED = [c for c in CASES if "_pis" not in c]
 
 
 @pytest.mark.parametrize("case", SUPPORTED)
@@ -55,7 +55,7 @@ def test_sample_points_match_oracle(case):
     np.testing.assert_allclose(tx[: int(f["n"])], f["tx"], rtol=0, atol=2e-5)
 
 
-@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2"])
+@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2", "gbm_mlp16_sdgd_K2"])
 def test_terminal_and_integral_estimators(case):
     f = load(case)
     eq = product_equation(f)
@@ -68,7 +68,7 @@ def test_terminal_and_integral_estimators(case):
     yT = gen.estimate_terminal_with_gradients(tx, point_base=pb).cpu().numpy()
     yI = gen.estimate_integral_with_gradients(tx, point_base=pb).cpu().numpy()
     _, rT, rI = O.labels_grad(oeq, onet, f["tx"], int(f["M"]), int(f["K"]), int(f["seed"]), int(f["epoch"]), pb,
-                              return_parts=True)
+                              v=int(f["v"]), return_parts=True)
     pT, pI = rel_l2_parts(yT, rT), rel_l2_parts(yI, rI)
     assert pT["value"] < TOL and pT["grad"] < TOL, pT
     assert pI["value"] < TOL and pI["grad"] < TOL, pI
@@ -114,6 +114,21 @@ def test_hjb_ou_mlp_vs_oracle():
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
+def test_gbm_config5_network_sdgd_vs_oracle():
+    """Config-5 network (3x64 ELU), SDGD v = 100, K = 50, against the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    net = _random_mlp(eq, [64] * 3, 6)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=50, seed=3, epoch=2,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": 100}})
+    tx, y = gen.sample_with_gradients(2)
+    oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+    ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 128, 50, 3, 2, 0, v=100)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
 def test_full_size_determinism_and_shard_invariance():
     """BASELINE config 2 size (16 x 4096 paths, K = 50): bitwise-reproducible labels, and moments
     computed as two MC shards + dpi_moments_reduce equal the single call bit for bit."""
@@ -154,6 +169,7 @@ def test_unsupported_configurations_fail_loudly():
     with pytest.raises(ValueError):
         dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(), 1, 1, device="cuda:0", t_always_uniform=True,
                                 n_estimate_terminal=100, n_estimate_integral=100)
-    with pytest.raises(DPIError):
-        dpi.construct_mlp  # noqa: B018
-        dpi.GBMEquationComplexExact(100).dpi_problem()
+    with pytest.raises(DPIError):  # GBM keeps all weights in LDS: hidden width <= 64
+        dpi.OnlineDataGenerator(dpi.GBMEquationComplexExact(100), dpi.construct_mlp(101, 1, [128] * 2, ["ELU"] * 2, None),
+                                1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                n_estimate_integral=64).sample_with_gradients(2)
