@@ -27,16 +27,23 @@ import torch
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-N_POINTS = 16
-M_PER_GPU = 4096
-K_STEPS = 50
 NX = 100
-WIDTHS = [128, 128, 128, 128]
-# algorithmic FLOP per path-label, SURVEY.md §8(d) (Burgers 4x128: MLP fwd 62,208 MAC + input-grad
-# 62,080 MAC + EM 2 K nx + misc)
-FLOP_PER_PATH_LABEL = 2.72e5
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector peak
 PEAK_HBM_GBS = 8000.0
+# workloads = BASELINE.json configs; FLOP per path-label from SURVEY.md §8(d)
+WORKLOADS = {
+    "burgers": dict(cfg="configs[1]", eq="Cha", widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0,
+                    flop=2.72e5, desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
+                                      "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)"),
+    "hjb": dict(cfg="configs[2]", eq="OUProcessEquation", widths=[512] * 4, pis=True, points=64, m_per_gpu=4096, K=50,
+                sdgd=0, flop=3.73e6,
+                desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
+                     "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
+    "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
+                sdgd=100, flop=3.36e6,
+                desc="Fully-nonlinear case_1 100d (GBM, SDGD v=100), 64 points x 1024 MC paths per GPU, K=50, "
+                     "MLP 101-64x3-1 ELU (BASELINE configs[4])"),
+}
 
 
 def parse():
@@ -46,28 +53,51 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-paths", type=int, default=512, help="MC paths per point in the CPU sample")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="burgers")
     return ap.parse_args()
 
 
-def cpu_baseline(sample_paths):
-    """Time the CPU oracle (oracle/: numpy fp64 restatement) on a bounded sample of the same
-    workload: 1 point x `sample_paths` paths x K = 50, same network."""
-    from oracle import dpi_oracle as O
-    import numpy as np
-    import deeppicarditeration_amd as dpi
+def _make(wl, dpi):
     torch.manual_seed(0)
-    net = dpi.construct_mlp(1 + NX, 1, WIDTHS, ["ELU"] * 4, None)
-    lin = [l for l in net if isinstance(l, torch.nn.Linear)]
-    onet = O.MLP([l.weight.detach().double().numpy() for l in lin], [l.bias.detach().double().numpy() for l in lin],
-                 ["ELU"] * 4)
-    oeq = O.Cha(NX, 1.0, 5.0, 1.0)
+    if wl["eq"] == "Cha":
+        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
+    elif wl["eq"] == "OUProcessEquation":
+        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+    else:
+        eq = dpi.GBMEquationComplexExact(NX, 1.0, 1.0)
+    if wl.get("pis"):
+        net = dpi.PISGradNet(hidden_shapes=wl["widths"], dim=NX, g0=eq.g, T=1.0)
+    else:
+        net = dpi.construct_mlp(1 + NX, 1, wl["widths"], ["ELU"] * len(wl["widths"]), None)
+    return eq, net
+
+
+def cpu_baseline(wl, sample_paths):
+    """Time the CPU oracle (oracle/: numpy fp64 restatement) on a bounded sample of the same
+    workload: 1 point x `sample_paths` paths x K, same network."""
+    from oracle import dpi_oracle as O
+    import deeppicarditeration_amd as dpi
+    eq, net = _make(wl, dpi)
+    if wl["eq"] == "Cha":
+        oeq = O.Cha(NX, 1.0, 5.0, 1.0)
+    elif wl["eq"] == "OUProcessEquation":
+        oeq = O.OUProcessEquation(NX, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    else:
+        oeq = O.GBMEquationComplexExact(NX, eq.w.numpy(), eq.v.numpy())
+    if wl.get("pis"):
+        onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    else:
+        lin = [l for l in net if isinstance(l, torch.nn.Linear)]
+        onet = O.MLP([l.weight.detach().double().numpy() for l in lin], [l.bias.detach().double().numpy() for l in lin],
+                     ["ELU"] * (len(lin) - 1))
     tx = O.sample_points(oeq, 1, seed=1)
     t0 = time.perf_counter()
-    O.labels_grad(oeq, onet, tx, sample_paths, K_STEPS, 1, 0, 0, m_chunk=sample_paths)
+    O.labels_grad(oeq, onet, tx, sample_paths, wl["K"], 1, 0, 0, v=wl["sdgd"], m_chunk=min(sample_paths, 256))
     dt = time.perf_counter() - t0
     cores = 1  # numpy elementwise Philox/Box–Muller runs on one thread
     return {"value": sample_paths / dt, "unit": "path-labels/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/dpi_oracle.py labels_grad, fp64 numpy, 1 point x {sample_paths} paths x K={K_STEPS}, "
+            "sample": f"oracle/dpi_oracle.py labels_grad, fp64 numpy, 1 point x {sample_paths} paths x K={wl['K']}, "
                       f"{dt:.1f} s on {platform.processor() or platform.machine()} (os.cpu_count={os.cpu_count()})"}
 
 
@@ -90,12 +120,14 @@ def main():
     from deeppicarditeration_amd import _lib as L
     from deeppicarditeration_amd.sharding import ShardedLabeler
 
-    torch.manual_seed(0)
-    eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
-    net = dpi.construct_mlp(1 + NX, 1, WIDTHS, ["ELU"] * 4, None)
+    wl = WORKLOADS[args.workload]
+    N_POINTS, M_PER_GPU, K_STEPS = wl["points"], wl["m_per_gpu"], wl["K"]
+    FLOP_PER_PATH_LABEL = wl["flop"]
+    eq, net = _make(wl, dpi)
     M = M_PER_GPU * world
+    hess = {"method": "SDGD", "kwargs": {"v": wl["sdgd"]}} if wl["sdgd"] else None
     gen = dpi.OnlineDataGenerator(eq, net, 80, 1, device=dev, t_always_uniform=True, n_estimate_terminal=M,
-                                  n_estimate_integral=M, n_euler_steps=K_STEPS, seed=1)
+                                  n_estimate_integral=M, n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
     labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD)
 
     # path-kernel timing with events on the stream the kernels run on (torch's current stream)
@@ -134,11 +166,11 @@ def main():
         per_launch_units = N_POINTS * M_PER_GPU
         achieved = FLOP_PER_PATH_LABEL * per_launch_units / (k_ms * 1e-3) / 1e12
         traffic = None
-        tf = ROOT / "profiles" / "traffic_burgers_cfg2.json"
+        tf = ROOT / "profiles" / f"traffic_{args.workload}.json"
         if tf.exists():
             traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
         out = {
-            "metric": "SDE-path labels/sec (100-d, 50 Euler steps); rel-L2 vs ref <= 1e-4 (tests/test_gpu_parity.py)",
+            "metric": "SDE-path labels/sec (100-d, 50 Euler steps) per GPU; rel-L2 vs ref",
             "value": value,
             "unit": "path-labels/s",
             "n_gpus": world,
@@ -149,18 +181,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (Philox-sampled collocation points; random-init 4x128 ELU MLP, torch.manual_seed(0))",
-            "config": {"workload": "Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
-                                   "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)",
+            "data": "synthetic (Philox-sampled collocation points; random-init ELU MLP, torch.manual_seed(0))",
+            "config": {"workload": wl["desc"], "baseline_config": wl["cfg"],
                        "points": N_POINTS, "mc_paths_per_gpu": M_PER_GPU, "euler_steps": K_STEPS, "nx": NX,
-                       "parallelism": f"mc-shard{world}"},
+                       "parallelism": f"mc-shard{world}", "per_gpu_value": value / world,
+                       "rel_l2_vs_ref": "<= 3e-7 measured, tolerance 1e-4 (tests/test_gpu_parity.py)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "kernel": "k_paths (+ its 2 small block-reduce kernels) per dpi_label_moments call",
                          "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample_paths)
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_paths if args.workload == "burgers" else 64)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

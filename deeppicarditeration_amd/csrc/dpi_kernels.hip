@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <type_traits>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -88,6 +89,11 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ g, int ncol
     *reinterpret_cast<float4*>(wsh + r * WST + 4 * c) = v;
   }
 }
+
+}  // namespace dpi
+#include "dpi_gemm.h"
+#include "dpi_pis.h"
+namespace dpi {
 
 // LDS layout (floats) shared by the baseline and path kernels.
 struct Lds {
@@ -941,7 +947,8 @@ struct dpi_problem_s {
 };
 
 struct dpi_net_s {
-  NetDev d;
+  NetDev d;        // d.kind: 0 zero, 1 mlp, 2 PISGradNet
+  NetPisDev pis;
   void* blob = nullptr;
   int n_in = 0;
 };
@@ -1173,6 +1180,153 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   return 0;
 }
 
+int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, const float* params, size_t n_params,
+                           dpi_net* out) {
+  if (!out || !hidden || !params || nx < 1 || nx > NXP_MAX || n_hidden < 1 || n_hidden > 4)
+    return fail(DPI_ERR_ARG, "pisgrad: bad arguments (1 <= n_hidden <= 4, nx <= 128)");
+  for (int l = 0; l < n_hidden; ++l)
+    if (hidden[l] < 4 || hidden[l] > 1024 || (hidden[l] % 4)) return fail(DPI_ERR_ARG, "pisgrad: hidden widths % 4");
+  const int C = PIS_CH, nsm = n_hidden, L = n_hidden, IN = C + nx;
+  // expected parameter count in state-dict order (solution.py:160-205)
+  size_t expect = 2 * C + (size_t)C * 2 * C + C + (size_t)C * C + C;   // phase, coeff, t_encoder
+  expect += (size_t)C * 2 * C + C + (size_t)nsm * (C * C + C) + (size_t)nx * C + nx;  // smooth_net
+  int in = IN;
+  for (int l = 0; l < L; ++l) {
+    expect += (size_t)hidden[l] * in + hidden[l];
+    in = hidden[l];
+  }
+  expect += (size_t)nx * in + nx;
+  if (n_params != expect) return fail(DPI_ERR_ARG, "pisgrad: parameter count mismatch");
+  const float* q = params;
+  auto take_src = [&](size_t cnt) {
+    const float* r = q;
+    q += cnt;
+    return r;
+  };
+  std::vector<float> blob;
+  auto put = [&](const float* src, size_t cnt) {
+    size_t off = blob.size();
+    blob.resize(off + ((cnt + 3) & ~size_t(3)), 0.f);
+    std::memcpy(blob.data() + off, src, cnt * sizeof(float));
+    return off;
+  };
+  auto putT = [&](const float* src, int rows, int cols, int c0, int nc) {  // (src[:, c0:c0+nc])^T
+    size_t off = blob.size();
+    blob.resize(off + (((size_t)nc * rows + 3) & ~size_t(3)), 0.f);
+    for (int r = 0; r < rows; ++r)
+      for (int c = 0; c < nc; ++c) blob[off + (size_t)c * rows + r] = src[(size_t)r * cols + c0 + c];
+    return off;
+  };
+  const float* phase = take_src(C);
+  const float* coeff = take_src(C);
+  const float* te0 = take_src((size_t)C * 2 * C);
+  const float* te0b = take_src(C);
+  const float* te2 = take_src((size_t)C * C);
+  const float* te2b = take_src(C);
+  const float* sn0 = take_src((size_t)C * 2 * C);
+  const float* sn0b = take_src(C);
+  const float *snw[4], *snbw[4];
+  for (int j = 0; j < nsm; ++j) {
+    snw[j] = take_src((size_t)C * C);
+    snbw[j] = take_src(C);
+  }
+  const float* snl = take_src((size_t)nx * C);
+  const float* snlb = take_src(nx);
+  const float *nnw[5], *nnbw[5];
+  int ins[5];
+  in = IN;
+  for (int l = 0; l <= L; ++l) {
+    const int o = l < L ? hidden[l] : nx;
+    nnw[l] = take_src((size_t)o * in);
+    nnbw[l] = take_src(o);
+    ins[l] = in;
+    in = o;
+  }
+  // smooth0 = smooth_net(emb(0))[0] in double on the host
+  double smooth0;
+  {
+    std::vector<double> e(2 * C), h(C), h2(C);
+    for (int j = 0; j < C; ++j) {
+      e[j] = std::sin((double)phase[j]);
+      e[C + j] = std::cos((double)phase[j]);
+    }
+    auto elu_d = [](double z) { return z > 0 ? z : std::expm1(z); };
+    for (int o = 0; o < C; ++o) {
+      double a = sn0b[o];
+      for (int k = 0; k < 2 * C; ++k) a += (double)sn0[(size_t)o * 2 * C + k] * e[k];
+      h[o] = a;
+    }
+    for (int j = 0; j < nsm; ++j) {
+      for (int o = 0; o < C; ++o) {
+        double a = snbw[j][o];
+        for (int k = 0; k < C; ++k) a += (double)snw[j][(size_t)o * C + k] * elu_d(h[k]);
+        h2[o] = a;
+      }
+      h.swap(h2);
+    }
+    double a = snlb[0];
+    for (int k = 0; k < C; ++k) a += (double)snl[k] * elu_d(h[k]);
+    smooth0 = a;
+  }
+  NetPisDev pd;
+  std::memset(&pd, 0, sizeof(pd));
+  size_t o_phase = put(phase, C), o_coeff = put(coeff, C), o_te0 = put(te0, (size_t)C * 2 * C), o_te0b = put(te0b, C),
+         o_te2 = put(te2, (size_t)C * C), o_te2b = put(te2b, C), o_sn0 = put(sn0, (size_t)C * 2 * C),
+         o_sn0b = put(sn0b, C), o_snl = put(snl, C), o_snlb = put(snlb, 1);
+  size_t o_sn[4], o_snb[4], o_nn[5], o_nnb[5], o_nnT[5];
+  for (int j = 0; j < nsm; ++j) {
+    o_sn[j] = put(snw[j], (size_t)C * C);
+    o_snb[j] = put(snbw[j], C);
+  }
+  for (int l = 0; l <= L; ++l) {
+    const int o = l < L ? hidden[l] : nx;
+    o_nn[l] = put(nnw[l], (size_t)o * ins[l]);
+    o_nnb[l] = put(nnbw[l], o);
+    o_nnT[l] = l == 0 ? putT(nnw[0], hidden[0], ins[0], C, nx) : putT(nnw[l], o, ins[l], 0, ins[l]);
+  }
+  auto* n = new dpi_net_s();
+  std::memset(&n->d, 0, sizeof(n->d));
+  void* d = nullptr;
+  if (hipMalloc(&d, blob.size() * sizeof(float)) != hipSuccess ||
+      hipMemcpy(d, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    if (d) (void)hipFree(d);
+    delete n;
+    return fail(DPI_ERR_HIP, "pisgrad: device upload failed");
+  }
+  const float* base = reinterpret_cast<const float*>(d);
+  pd.nx = nx;
+  pd.L = L;
+  pd.nsm = nsm;
+  for (int l = 0; l < L; ++l) pd.h[l] = hidden[l];
+  pd.T = (float)T;
+  pd.smooth0 = (float)smooth0;
+  pd.phase = base + o_phase;
+  pd.coeff = base + o_coeff;
+  pd.te0 = base + o_te0;
+  pd.te0b = base + o_te0b;
+  pd.te2 = base + o_te2;
+  pd.te2b = base + o_te2b;
+  pd.sn0 = base + o_sn0;
+  pd.sn0b = base + o_sn0b;
+  for (int j = 0; j < nsm; ++j) {
+    pd.sn[j] = base + o_sn[j];
+    pd.snb[j] = base + o_snb[j];
+  }
+  pd.snlast = base + o_snl;
+  pd.snlastb = base + o_snlb;
+  for (int l = 0; l <= L; ++l) {
+    pd.nn[l] = base + o_nn[l];
+    pd.nnb[l] = base + o_nnb[l];
+    pd.nnT[l] = base + o_nnT[l];
+  }
+  n->blob = d;
+  n->n_in = 1 + nx;
+  n->d.kind = 2;
+  n->pis = pd;
+  *out = n;
+  return 0;
+}
+
 int dpi_net_destroy(dpi_net net) {
   if (!net) return 0;
   if (net->blob) (void)hipFree(net->blob);
@@ -1182,22 +1336,121 @@ int dpi_net_destroy(dpi_net net) {
 
 }  // extern "C"
 
-// Workspace: gx[n] | fb[n] | bx[n][H] | partial[n][nbp][2][F]   (256-B aligned pieces)
+// PISGradNet pipeline rows (floats per path) and chunking
+static PisRows pis_rows_layout(const NetPisDev& pd) {
+  auto r4 = [](int x) { return (x + 3) & ~3; };
+  int hmax = 0;
+  for (int l = 0; l < pd.L; ++l) hmax = std::max(hmax, pd.h[l]);
+  PisRows L;
+  int o = 0;
+  L.E = o;
+  o += 2 * PIS_CH;
+  L.T1 = o;
+  o += PIS_CH;
+  L.IN = o;
+  o += r4(PIS_CH + pd.nx);
+  L.H0 = o;
+  o += PIS_CH;
+  L.H1 = o;
+  o += PIS_CH;
+  for (int l = 0; l < 4; ++l) {
+    L.A[l] = o;
+    o += l < pd.L ? r4(pd.h[l]) : 0;
+  }
+  L.NO = o;
+  o += r4(pd.nx);
+  L.D0 = o;
+  o += r4(hmax);
+  L.D1 = o;
+  o += r4(hmax);
+  L.GX = o;
+  o += r4(pd.nx);
+  L.SS = o;
+  o += r4(pd.nx);
+  L.ST = o;
+  o += r4(pd.nx);
+  L.SC = o;
+  o += 4;
+  L.stride = o;
+  return L;
+}
+constexpr int PIS_CHUNK_WG = 512;  // (point, 64-path block) pairs per pipeline chunk = 32,768 rows
+
+// Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | [PIS rows] | partial[n][2F][nbp]  (256-B aligned)
 struct WsLayout {
-  size_t gx, fb, bx, hb, partial, total;
+  size_t gx, fb, bx, hb, rows, partial, total;
+  int rows_cap;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   WsLayout w;
-  const int H = (net && net->d.kind) ? net->d.H : 0;
+  const int H = (net && net->d.kind == 1) ? net->d.H : 0;
   const size_t nbp = (size_t)(M + P - 1) / P;
   w.gx = 0;
   w.fb = al256((size_t)n * 4);
   w.bx = w.fb + al256((size_t)n * 4);
   w.hb = w.bx + al256((size_t)n * H * 4);
-  w.partial = w.hb + al256((size_t)n * NXP_MAX * 4);
+  w.rows = w.hb + al256((size_t)n * NXP_MAX * 4);
+  w.rows_cap = 0;
+  size_t rows_bytes = 0;
+  if (net && net->d.kind == 2) {
+    const size_t need = std::max((size_t)n, (size_t)n * nbp * P);
+    w.rows_cap = (int)std::min(need, (size_t)PIS_CHUNK_WG * P);
+    w.rows_cap = std::max(w.rows_cap, (int)std::min((size_t)n, (size_t)PIS_CHUNK_WG * P));
+    rows_bytes = al256((size_t)w.rows_cap * pis_rows_layout(net->pis).stride * 4);
+  }
+  w.partial = w.rows + rows_bytes;
   w.total = w.partial + (size_t)n * nbp * 2 * F * 4;
   return w;
+}
+
+static void gemm(int epi, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                 const float* bias, const float* aux, int ldaux, hipStream_t st) {
+  dim3 grid((M + GBM_ - 1) / GBM_, (N + GBN_ - 1) / GBN_), block(256);
+  if (epi == EPI_BIAS)
+    hipLaunchKernelGGL(k_gemm_nt<EPI_BIAS>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux);
+  else if (epi == EPI_BIAS_ELU)
+    hipLaunchKernelGGL(k_gemm_nt<EPI_BIAS_ELU>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux);
+  else
+    hipLaunchKernelGGL(k_gemm_nt<EPI_DELU>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux);
+}
+
+// PISGradNet forward + VJP over R rows (solution.py:256-289); returns the row layout with H0 pointing
+// at the last smooth_net activation.
+static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st) {
+  PisRows L = pis_rows_layout(pd);
+  const int ld = L.stride, C = PIS_CH, nx = pd.nx;
+  // t_encoder -> IN[:, 0:64]
+  gemm(EPI_BIAS_ELU, R, C, 2 * C, rows + L.E, ld, pd.te0, 2 * C, rows + L.T1, ld, pd.te0b, nullptr, 0, st);
+  gemm(EPI_BIAS, R, C, C, rows + L.T1, ld, pd.te2, C, rows + L.IN, ld, pd.te2b, nullptr, 0, st);
+  // smooth_net hidden activations (elu applied on store: each is consumed through an ELU)
+  int hs = L.H0, ho = L.H1;
+  gemm(EPI_BIAS_ELU, R, C, 2 * C, rows + L.E, ld, pd.sn0, 2 * C, rows + hs, ld, pd.sn0b, nullptr, 0, st);
+  for (int j = 0; j < pd.nsm; ++j) {
+    gemm(EPI_BIAS_ELU, R, C, C, rows + hs, ld, pd.sn[j], C, rows + ho, ld, pd.snb[j], nullptr, 0, st);
+    std::swap(hs, ho);
+  }
+  // nn_module forward
+  int in = C + nx;
+  const float* a = rows + L.IN;
+  for (int l = 0; l < pd.L; ++l) {
+    gemm(EPI_BIAS_ELU, R, pd.h[l], in, a, ld, pd.nn[l], in, rows + L.A[l], ld, pd.nnb[l], nullptr, 0, st);
+    a = rows + L.A[l];
+    in = pd.h[l];
+  }
+  gemm(EPI_BIAS, R, nx, in, a, ld, pd.nn[pd.L], in, rows + L.NO, ld, pd.nnb[pd.L], nullptr, 0, st);
+  // VJP with cotangent X on net_out: D_{L-1} = (X nn_L) * elu'(A_{L-1}), ..., GX = D_0 nn_0[:, 64:]
+  int dcur = L.D0, dnext = L.D1;
+  gemm(EPI_DELU, R, pd.h[pd.L - 1], nx, rows + L.IN + PIS_IN_OFF, ld, pd.nnT[pd.L], nx, rows + dcur, ld, nullptr,
+       rows + L.A[pd.L - 1], ld, st);
+  for (int l = pd.L - 1; l >= 1; --l) {
+    gemm(EPI_DELU, R, pd.h[l - 1], pd.h[l], rows + dcur, ld, pd.nnT[l], pd.h[l], rows + dnext, ld, nullptr,
+         rows + L.A[l - 1], ld, st);
+    std::swap(dcur, dnext);
+  }
+  gemm(EPI_BIAS, R, nx, pd.h[0], rows + dcur, ld, pd.nnT[0], pd.h[0], rows + L.GX, ld, nullptr, nullptr, 0, st);
+  L.H0 = hs;
+  return L;
 }
 
 extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) {
@@ -1318,6 +1571,52 @@ static int check_pair(dpi_problem p, dpi_net net) {
   return 0;
 }
 
+static int pis_check(dpi_problem p) {
+  if (p->e.kind != DPI_EQ_OU)
+    return fail(DPI_ERR_UNSUPPORTED, "PISGradNet device net needs OUProcessEquation (its g0 is the problem's GMM g)");
+  return 0;
+}
+
+static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, const WsLayout& w, char* b,
+                        hipStream_t st) {
+  int rc = pis_check(p);
+  if (rc) return rc;
+  float *gx = (float*)(b + w.gx), *fb = (float*)(b + w.fb), *rows = (float*)(b + w.rows);
+  // g(x) (k_baseline's zero-net instance also writes a placeholder f_b, overwritten below)
+  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTH), 0, st, p->e, net->d, tx, n, gx, fb,
+                     (float*)(b + w.bx), (float*)(b + w.hb));
+  const int F = 1 + p->e.nx;
+  const PisRows L = pis_rows_layout(net->pis);
+  for (int i0 = 0; i0 < n; i0 += w.rows_cap) {
+    const int R = std::min(w.rows_cap, n - i0);
+    hipLaunchKernelGGL(k_pis_points, dim3(R), dim3(64), 0, st, p->e.nx, net->pis, tx + (size_t)i0 * F, R, rows, L);
+    const PisRows Lc = pis_chain(net->pis, rows, R, st);
+    hipLaunchKernelGGL(k_pis_base_final<DPI_EQ_OU>, dim3((R + 15) / 16), dim3(64), 0, st, p->e, net->pis, rows, Lc,
+                       R, fb + i0);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
+                     char* b, hipStream_t st) {
+  int rc = pis_check(p);
+  if (rc) return rc;
+  float* rows = (float*)(b + w.rows);
+  const PisRows L = pis_rows_layout(net->pis);
+  const int G = n * a.nbp, GC = std::max(1, w.rows_cap / P);
+  for (int g0 = 0; g0 < G; g0 += GC) {
+    const int g = std::min(GC, G - g0);
+    hipLaunchKernelGGL(k_pis_rollout<DPI_EQ_OU>, dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, a.m_begin,
+                       K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L);
+    const PisRows Lc = pis_chain(net->pis, rows, g * P, st);
+    hipLaunchKernelGGL(k_pis_final<DPI_EQ_OU>, dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K, a.flags,
+                       a.fb, rows, Lc, a.partial);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes, void* stream) {
   int rc = check_pair(p, net);
   if (rc) return rc;
@@ -1326,6 +1625,7 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
   if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
+  if (net->d.kind == 2) return pis_baseline(p, net, tx, n, w, b, (hipStream_t)stream);
   Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), nullptr, 0,
            (hipStream_t)stream};
   if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "point_baseline: unsupported equation/network shape");
@@ -1369,8 +1669,13 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.point_base = point_base;
   hipStream_t st = (hipStream_t)stream;
-  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
-  if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
+  if (net->d.kind == 2) {
+    if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st))) return rc;
+  } else {
+    Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
+    if (!dispatch_any(p, net, q))
+      return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
+  }
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
                      (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y);

@@ -151,4 +151,29 @@ class DeviceNet:
                                               flat.ctypes.data_as(_lib.P(_lib.c_float)), flat.size, h),
                        "dpi_net_create_mlp")
             return cls(h, f"mlp{widths}")
+        if isinstance(m, PISGradNet) or type(m).__name__ == "PISGradNet":
+            return cls._from_pisgrad(lib, m, n_in)
         raise NotImplementedError(f"network type {type(m).__name__} has no device implementation in this build")
+
+    @classmethod
+    def _from_pisgrad(cls, lib, m, n_in):
+        """PISGradNet -> dpi_net_create_pisgrad (state-dict order, solution.py:160-205)."""
+        nx = n_in - 1
+        if m.dim != nx or m.channels != 64:
+            raise ValueError("PISGradNet dim/channels mismatch")
+        g0_owner = getattr(m.g0, "__self__", None)
+        if g0_owner is None or type(g0_owner).__name__ != "OUProcessEquation":
+            raise NotImplementedError("PISGradNet on the device needs g0 = OUProcessEquation.g (as PicardSolution builds it)")
+        sd = m.state_dict()
+        L = len(m.hidden_shapes)
+        names = ["timestep_phase", "timestep_coeff", "t_encoder.0.weight", "t_encoder.0.bias", "t_encoder.2.weight",
+                 "t_encoder.2.bias"]
+        names += [f"smooth_net.{2 * j}.{w}" for j in range(L + 2) for w in ("weight", "bias")]
+        names += [f"nn_module.{2 * l}.{w}" for l in range(L + 1) for w in ("weight", "bias")]
+        flat = np.ascontiguousarray(np.concatenate([sd[k].detach().cpu().double().numpy().ravel() for k in names]),
+                                    np.float32)
+        hidden = (_lib.c_int * L)(*[int(h) for h in m.hidden_shapes])
+        h = _lib.c_void_p()
+        _lib.check(lib.dpi_net_create_pisgrad(nx, L, hidden, float(m.T), flat.ctypes.data_as(_lib.P(_lib.c_float)),
+                                              flat.size, h), "dpi_net_create_pisgrad")
+        return cls(h, f"pisgrad{list(m.hidden_shapes)}")

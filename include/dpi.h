@@ -15,6 +15,7 @@
  *   dpi_problem_set_hessian_approximation  picard/data.py:115-123, :497-502  HESSIAN_APPROXIMATION (SDGD v)
  *   dpi_net_create_zero      picard/solution.py:330-337   ZeroSolution (iteration 1)
  *   dpi_net_create_mlp       picard/solution.py:123-135   construct_mlp (state-dict order)
+ *   dpi_net_create_pisgrad   picard/solution.py:138-289   PISGradNet (state-dict order)
  *   dpi_sample_points        picard/data.py:161-167, :211-217  sample_t_always_uniform + equation.sample_x
  *   dpi_point_baseline       picard/data.py:506-518, :918-920  g(x) and get_f(..., baseline_repeat=M)
  *   dpi_label_moments        picard/data.py:899-926 + :471-527 (+ :1226-1325 get_f) summed over MC paths
@@ -98,6 +99,11 @@ int dpi_net_create_zero(dpi_net* out);
  * (GBM: width <= 64). */
 int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params,
                        size_t n_params, dpi_net* out);
+/* PISGradNet(hidden_shapes, dim = nx, g0 = equation.g, T) for OUProcessEquation; params: host fp32 in
+ * torch state-dict order (timestep_phase, timestep_coeff, t_encoder.{0,2}, smooth_net.{0,2,..,2(L+1)},
+ * nn_module.{0,2,..,2L} weights and biases).  Runs as a layer-wise MFMA GEMM pipeline. */
+int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, const float* params,
+                           size_t n_params, dpi_net* out);
 int dpi_net_destroy(dpi_net net);
 
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */

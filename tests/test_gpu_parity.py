@@ -26,7 +26,7 @@ from golden_util import CASES, load, oracle_equation, oracle_net  # noqa: E402
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
-SUPPORTED = [c for c in CASES if "_pis" not in c]
+SUPPORTED = list(CASES)
 
 
 @pytest.mark.parametrize("case", SUPPORTED)
@@ -125,6 +125,25 @@ def test_gbm_config5_network_sdgd_vs_oracle():
     tx, y = gen.sample_with_gradients(2)
     oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
     ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 128, 50, 3, 2, 0, v=100)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_hjb_pisgradnet_config3_network_vs_oracle():
+    """Config-3 network: PISGradNet 4 x 512 (layer-wise MFMA GEMM pipeline), OU + GMM, K = 20."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(7)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    with torch.no_grad():
+        net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=20, seed=2, epoch=1)
+    tx, y = gen.sample_with_gradients(2)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 20, 2, 1, 0)
     parts = rel_l2_parts(y.cpu().numpy(), ref)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
