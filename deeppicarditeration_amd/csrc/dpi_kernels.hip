@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <type_traits>
 #include <algorithm>
 #include <string>
@@ -1404,9 +1405,31 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   return w;
 }
 
+// GEMM precision: exact-fp32 MFMA by default; DPI_GEMM=f16x3 selects the fp16-split kernel
+// (same speed today: both are load-latency bound).
+static bool gemm_f32() {
+  static const bool v = [] {
+    const char* e = std::getenv("DPI_GEMM");
+    return !(e && std::strcmp(e, "f16x3") == 0);
+  }();
+  return v;
+}
+
 static void gemm(int epi, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
                  const float* bias, const float* aux, int ldaux, hipStream_t st) {
   dim3 grid((M + GBM_ - 1) / GBM_, (N + GBN_ - 1) / GBN_), block(256);
+  if (!gemm_f32()) {
+    if (epi == EPI_BIAS)
+      hipLaunchKernelGGL(k_gemm_nt_f16x3<EPI_BIAS>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux,
+                         ldaux);
+    else if (epi == EPI_BIAS_ELU)
+      hipLaunchKernelGGL(k_gemm_nt_f16x3<EPI_BIAS_ELU>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux,
+                         ldaux);
+    else
+      hipLaunchKernelGGL(k_gemm_nt_f16x3<EPI_DELU>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux,
+                         ldaux);
+    return;
+  }
   if (epi == EPI_BIAS)
     hipLaunchKernelGGL(k_gemm_nt<EPI_BIAS>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux);
   else if (epi == EPI_BIAS_ELU)
