@@ -36,6 +36,7 @@ SIGNATURES = {
     "dpi_net_create_mlp": (c_int, [c_int, c_int, P(c_int), c_int, P(c_float), c_size_t, P(c_void_p)]),
     "dpi_net_create_pisgrad": (c_int, [c_int, c_int, P(c_int), c_double, P(c_float), c_size_t, P(c_void_p)]),
     "dpi_net_destroy": (c_int, [c_void_p]),
+    "dpi_set_gemm_precision": (c_int, [c_int]),
     "dpi_workspace_bytes": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_sample_points": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_void_p, c_void_p]),
     "dpi_point_baseline": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),

@@ -1407,12 +1407,19 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
 
 // GEMM precision: exact-fp32 MFMA by default; DPI_GEMM=f16x3 selects the fp16-split kernel
 // (same speed today: both are load-latency bound).
+static int g_gemm_mode = -1;  // -1: from the environment, 0: fp32, 1: fp16-split
 static bool gemm_f32() {
-  static const bool v = [] {
+  if (g_gemm_mode < 0) {
     const char* e = std::getenv("DPI_GEMM");
-    return !(e && std::strcmp(e, "f16x3") == 0);
-  }();
-  return v;
+    g_gemm_mode = (e && std::strcmp(e, "f16x3") == 0) ? 1 : 0;
+  }
+  return g_gemm_mode == 0;
+}
+
+extern "C" int dpi_set_gemm_precision(int mode) {
+  if (mode != 0 && mode != 1) return fail(DPI_ERR_ARG, "gemm precision: 0 = fp32, 1 = fp16-split");
+  g_gemm_mode = mode;
+  return 0;
 }
 
 static void gemm(int epi, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C, int ldc,

@@ -106,6 +106,10 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
                            size_t n_params, dpi_net* out);
 int dpi_net_destroy(dpi_net net);
 
+/* MFMA precision of the layer-wise GEMM pipeline (PISGradNet): 0 = exact fp32 (default),
+ * 1 = fp16-split x = hi + 2^-11 lo, three f16 MFMAs per product (~2.4e-7 relative error). */
+int dpi_set_gemm_precision(int mode);
+
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
 size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
 

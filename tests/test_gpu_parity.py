@@ -129,9 +129,13 @@ def test_gbm_config5_network_sdgd_vs_oracle():
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-def test_hjb_pisgradnet_config3_network_vs_oracle():
-    """Config-3 network: PISGradNet 4 x 512 (layer-wise MFMA GEMM pipeline), OU + GMM, K = 20."""
+@pytest.mark.parametrize("gemm_mode", [0, 1])
+def test_hjb_pisgradnet_config3_network_vs_oracle(gemm_mode):
+    """Config-3 network: PISGradNet 4 x 512 (layer-wise MFMA GEMM pipeline, fp32 and fp16-split),
+    OU + GMM, K = 20."""
     import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    L.check(L.load().dpi_set_gemm_precision(gemm_mode), "gemm precision")
     eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
                                alpha_scale=4.0)
     torch.manual_seed(7)
@@ -144,7 +148,9 @@ def test_hjb_pisgradnet_config3_network_vs_oracle():
     oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
     onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
     ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 20, 2, 1, 0)
+    L.check(L.load().dpi_set_gemm_precision(0), "gemm precision")
     parts = rel_l2_parts(y.cpu().numpy(), ref)
+    print("gemm mode", gemm_mode, parts)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
