@@ -17,6 +17,7 @@ DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
 DPI_ACT_ELU = 1
 DPI_TERMINAL, DPI_INTEGRAL, DPI_BOTH = 1, 2, 3
 DPI_PATH_BLOCK = 64
+DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
 
 c_int, c_double, c_float, c_size_t, c_void_p, c_uint32, c_uint64 = (
     ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64)

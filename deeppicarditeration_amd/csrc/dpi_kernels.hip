@@ -59,6 +59,12 @@ struct NetDev {
   const float* b[4];
   const float* wout;  // (H)
   float bout;
+  // fp16-split copies (x = hi + 2^-11 lo) in MFMA fragment order, see pack_split():
+  int nxp32;                 // nx padded to 32
+  const uint32_t* W1xS;      // (H, nxp32)
+  const uint32_t* W1xTS;     // (nxp32, H)
+  const uint32_t* WS[4];     // (H, H)
+  const uint32_t* WTS[4];
 };
 
 // ------------------------------------------------------------------------------ helpers
@@ -89,6 +95,73 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ g, int ncol
     const float4 v = *reinterpret_cast<const float4*>(g + (size_t)(r0 + r) * ncol + 4 * c);
     *reinterpret_cast<float4*>(wsh + r * WST + 4 * c) = v;
   }
+}
+
+// ---------------- fp16-split MFMA (v_mfma_f32_16x16x32_f16, three products per fp32 product)
+// x = hi + 2^-11 lo with hi = fp16(x), lo = fp16((x - hi) 2^11): a (x) b = hi_a hi_b + 2^-11 (hi_a lo_b
+// + lo_a hi_b) + O(2^-22 |a b|).  Split matrices are packed per row as chunks of 32 columns; chunk
+// u holds, for each lane group q = 0..3, 8 hi then 8 lo halves of columns
+// k(q, j) = 32u + 4q + (j & 3) + 16 (j >> 2), j = 0..7 — exactly the columns whose activations a
+// lane of group q holds in the 16x16 C layout of tiles 2u and 2u+1, so activations become the B
+// operand without any data movement.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
+constexpr float SPLIT_LO = 2048.0f, SPLIT_INV = 1.0f / 2048.0f;
+
+__device__ __forceinline__ floatx4 mfma16(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split8(const float (&x)[8], half8& hi, half8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)x[j];
+    hi[j] = h;
+    lo[j] = (_Float16)((x[j] - (float)h) * SPLIT_LO);
+  }
+}
+// B operand of chunk u from activation tiles 2u, 2u+1 held in the C layout.
+__device__ __forceinline__ void split_act(const float (&t0)[4], const float (&t1)[4], half8& hi, half8& lo) {
+  const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  split8(x, hi, lo);
+}
+// Stage rows [r0, r0 + nrows) of a split-packed matrix (C words per row) into LDS rows of C + 4
+// words (C + 4 = 4 mod 64 or 36 mod 64 words: the 16 rows of a ds_read_b128 hit distinct banks).
+__device__ __forceinline__ void stage_rows_split(const uint32_t* __restrict__ g, int C, int r0, int nrows,
+                                                 uint32_t* wsh) {
+  const int n4 = C >> 2, st = C + 4;
+  for (int idx = threadIdx.x; idx < nrows * n4; idx += NTH) {
+    const int r = idx / n4, c = idx - r * n4;
+    const u32v4 v = *reinterpret_cast<const u32v4*>(g + (size_t)(r0 + r) * C + 4 * c);
+    *reinterpret_cast<u32v4*>(wsh + r * st + 4 * c) = v;
+  }
+}
+__device__ __forceinline__ void load_a_split(const uint32_t* wsh, int st, int row, int u, int q, half8& ah,
+                                             half8& al) {
+  const uint32_t* p = wsh + row * st + u * 32 + q * 8;
+  ah = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(p));
+  al = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(p + 4));
+}
+// 32 output rows (tiles T0, T0+1) of W B for a staged 32-row chunk; B pre-split per chunk u.
+template <int NU>
+__device__ __forceinline__ void split_rows32(const uint32_t* wsh, int st, int jj, int qq, const half8 (&bh)[NU],
+                                             const half8 (&bl)[NU], floatx4 (&out)[2]) {
+  floatx4 am[2], ac[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      half8 ah, al;
+      load_a_split(wsh, st, 16 * t + jj, u, qq, ah, al);
+      am[t] = mfma16(ah, bh[u], am[t]);
+      ac[t] = mfma16(ah, bl[u], ac[t]);
+      ac[t] = mfma16(al, bh[u], ac[t]);
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[t][r] = fmaf(ac[t][r], SPLIT_INV, am[t][r]);
 }
 
 }  // namespace dpi
@@ -269,6 +342,141 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
           }
         }
       }
+    }
+    gA_out = qsum(A);
+    gB_out = qsum(B);
+    gsum_out = 0.f;
+  }
+}
+
+// mlp_tile on the fp16-split MFMA (H % 32 == 0): same inputs, outputs and tile layout; each
+// 16x16x4 f32 chain becomes 16x16x32 f16 chunks (3 MFMAs per 32-wide chunk instead of 8), the
+// weights come pre-split from NetDev::*S, the activations are split in registers.
+template <int KIND, int H, int L, class SH>
+__device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net, SH& sh, float& u_out,
+                                               float& gsum_out, float& gA_out, float& gB_out) {
+  static_assert(H % 32 == 0, "split MLP needs H % 32 == 0");
+  constexpr int HT = H / 16, NU = H / 32;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  uint32_t* wsh = reinterpret_cast<uint32_t*>(sh.W);
+  const int C1 = net.nxp32, nu1 = C1 >> 5;
+  float act[L][HT][4];
+  half8 bh[NU], bl[NU];
+
+  // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+#pragma unroll
+  for (int T0 = 0; T0 < HT; T0 += 2) {
+    __syncthreads();
+    stage_rows_split(net.W1xS, C1, 16 * T0, 32, wsh);
+    __syncthreads();
+    floatx4 am[2], ac[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < nu1; ++u) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = sh.S[(32 * u + 4 * qq + (j & 3) + 16 * (j >> 2)) * SS + pp];
+      half8 xh, xl;
+      split8(x, xh, xl);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        half8 ah, al;
+        load_a_split(wsh, C1 + 4, 16 * t + jj, u, qq, ah, al);
+        am[t] = mfma16(ah, xh, am[t]);
+        ac[t] = mfma16(ah, xl, ac[t]);
+        ac[t] = mfma16(al, xh, ac[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * (T0 + t) + 4 * qq + r;
+        const float acc = fmaf(ac[t][r], SPLIT_INV, am[t][r]);
+        act[0][T0 + t][r] = elu(fmaf(cm, acc, fmaf(sh.vec[H + h], tau, sh.vec[h])));
+      }
+  }
+  // ---------------- hidden layers
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[l - 1][2 * u], act[l - 1][2 * u + 1], bh[u], bl[u]);
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      __syncthreads();
+      stage_rows_split(net.WS[l], H, 16 * T0, 32, wsh);
+      __syncthreads();
+      floatx4 o[2];
+      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = elu(o[t][r] + sh.bh[l * H + 16 * (T0 + t) + 4 * qq + r]);
+    }
+  }
+  // ---------------- output u = wout . a_L + bout ; delta_L = wout * elu'(a_L)
+  float up = 0.f;
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      const float w = sh.vec[2 * H + h];
+      up = fmaf(w, act[L - 1][T][r], up);
+      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+    }
+  u_out = qsum(up) + net.bout;
+  // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[l + 1][2 * u], act[l + 1][2 * u + 1], bh[u], bl[u]);
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      __syncthreads();
+      stage_rows_split(net.WTS[l + 1], H, 16 * T0, 32, wsh);
+      __syncthreads();
+      floatx4 o[2];
+      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = o[t][r] * delu_from_a(act[l][T0 + t][r]);
+    }
+  }
+  // ---------------- input gradient
+  if (!Eq<KIND>::GRAD_FULL) {
+    float gp = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp = fmaf(sh.vec[3 * H + 16 * T + 4 * qq + r], act[0][T][r], gp);
+    gsum_out = qsum(gp);
+    gA_out = gB_out = 0.f;
+  } else {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[0][2 * u], act[0][2 * u + 1], bh[u], bl[u]);
+    float A = 0.f, B = 0.f;
+    for (int T0 = 0; T0 < (C1 >> 4); T0 += 2) {
+      __syncthreads();
+      stage_rows_split(net.W1xTS, H, 16 * T0, 32, wsh);
+      __syncthreads();
+      floatx4 o[2];
+      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = 16 * (T0 + t) + 4 * qq + r;
+          if (d < e.nx) {
+            const float X = fmaf(cm, sh.S[d * SS + pp], sh.xsh[d]);
+            Eq<KIND>::gacc(e, d, X, o[t][r], A, B);
+          }
+        }
     }
     gA_out = qsum(A);
     gB_out = qsum(B);
@@ -614,10 +822,12 @@ struct PathArgs {
   float* partial;
   int n, nbp, m_begin, K, flags;
   uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
+  int order;  // phase order policy (k_paths)
+  int split;  // fused MLP on the fp16-split MFMA
 };
 
 // One workgroup = (point i, 64 consecutive MC indices).  See the file header.
-template <int KIND, int H, int L, bool ZERO>
+template <int KIND, int H, int L, bool ZERO, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
@@ -637,7 +847,8 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   const float Kf = (float)a.K;
 
   for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
-  for (int idx = tid; idx < (nxp - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
+  const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
+  for (int idx = tid; idx < (nxpz - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
     const int d = 4 * nb + idx / P, p = idx % P;
     sh.S[d * SS + p] = 0.f;
   }
@@ -680,7 +891,7 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   // s ~ U(t, T] for this lane's path (data.py:359); integral/terminal step multipliers
   const float U = u01_oc(philox4x32_10(0u, m, ig, a.c3s, a.k0, a.k1).x);
   const float s = fmaf(U, tmt, t);
-  const float smt = s - t;
+  const float smt = U * tmt;  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
   const float cI = e.asq * sqrtf(smt / Kf);            // X_s = x + cI * sum_k xi_k
   const float yI = 1.0f / (sqrtf(Kf * smt) * e.asq);    // Y_s = yI * sum_k xi_k   (data.py:520)
   const float cT = e.asq * sqrtf(tmt / Kf);
@@ -715,119 +926,161 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
       }
     }
   }
+  auto terminal_rollout = [&]() {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int j = wv + 4 * c;  // terminal dim-blocks of this wave
-    ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
-    if (TERM && j < nb) {
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      for (int k = 0; k < a.K; ++k) {
-        const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
-        s0 += z.a;
-        s1 += z.b;
-        s2 += z.c;
-        s3 += z.d;
-      }
-      ST[c][0] = s0 * BM_SCALE;
-      ST[c][1] = s1 * BM_SCALE;
-      ST[c][2] = s2 * BM_SCALE;
-      ST[c][3] = s3 * BM_SCALE;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * j + q;
-        if (d < nx) Eq<KIND>::gstat(e, d, fmaf(cT, ST[c][q], sh.xsh[d]), gst);
-      }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
-    if (j < nb) {
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      if (INTG) {
+    for (int c = 0; c < 8; ++c) {
+      const int j = wv + 4 * c;  // terminal dim-blocks of this wave
+      ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
+      if (TERM && j < nb) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         for (int k = 0; k < a.K; ++k) {
-          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
+          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
           s0 += z.a;
           s1 += z.b;
           s2 += z.c;
           s3 += z.d;
         }
+        ST[c][0] = s0 * BM_SCALE;
+        ST[c][1] = s1 * BM_SCALE;
+        ST[c][2] = s2 * BM_SCALE;
+        ST[c][3] = s3 * BM_SCALE;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          if (d < nx) Eq<KIND>::gstat(e, d, fmaf(cT, ST[c][q], sh.xsh[d]), gst);
+        }
       }
-      const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+    }
+  };
+  auto integral_rollout = [&]() {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * j + q;
-        sh.S[d * SS + lane] = d < nx ? sv[q] : 0.f;
-        if constexpr (GBM) {  // w_k . S for the exact-solution terms at X_s = x + cI S
-          if (d < nx) {
+    for (int c = 0; c < 8; ++c) {
+      const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
+      if (j < nb) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (INTG) {
+          for (int k = 0; k < a.K; ++k) {
+            const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
+            s0 += z.a;
+            s1 += z.b;
+            s2 += z.c;
+            s3 += z.d;
+          }
+        }
+        const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
 #pragma unroll
-            for (int c = 0; c < NSG; ++c)
-              if (c < e.nodes) fst[c] = fmaf(e.gw[c * F + 1 + d], sv[q], fst[c]);
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          sh.S[d * SS + lane] = d < nx ? sv[q] : 0.f;
+          if constexpr (GBM) {  // w_k . S for the exact-solution terms at X_s = x + cI S
+            if (d < nx) {
+#pragma unroll
+              for (int c = 0; c < NSG; ++c)
+                if (c < e.nodes) fst[c] = fmaf(e.gw[c * F + 1 + d], sv[q], fst[c]);
+            }
           }
         }
       }
     }
-  }
+  };
+  // g(X_T) statistics over the 4 waves in fixed order; the barrier also publishes S / fst
+  auto terminal_finish = [&]() -> float {
 #pragma unroll
-  for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = gst[c];
-  if constexpr (GBM) {
+    for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = gst[c];
+    if constexpr (GBM) {
 #pragma unroll
-    for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fst[c];
-  }
-  __syncthreads();
-  float gT = 0.f;
-  if (TERM) {
+      for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fst[c];
+    }
+    __syncthreads();
+    float gT = 0.f;
+    if (TERM) {
 #pragma unroll
-    for (int c = 0; c < NSG; ++c)
-      gst[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
-                sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
-    gT = Eq<KIND>::gfin(e, gst);
-  }
-  const float ap = TERM ? gT - g_x : 0.f;  // (g(X_T) - g(x)) (data.py:923)
+      for (int c = 0; c < NSG; ++c)
+        gst[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
+                  sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
+      gT = Eq<KIND>::gfin(e, gst);
+    }
+    return TERM ? gT - g_x : 0.f;  // (g(X_T) - g(x)) (data.py:923)
+  };
 
-  // ---------------- phase 2: u, grad u (or the SDGD Hessian diagonal) at (s, X_s) and f
-  if constexpr (!GBM) {
-    float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
-    if (!ZERO && INTG) mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
-    const int pp = 16 * wv + (lane & 15);
-    if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
-  } else {
-    // ffi (equations.py:457-466) with u_ii from SDGD (data.py:1273-1303); the baseline f_b
-    // gathers the point's Hessian diagonal at this path's indices (data.py:1293-1302).
-    const int jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
-    float s1 = 0.f, s2 = 0.f;
-    if (!ZERO && INTG) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
-    const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
-    const float c1 = 0.5f * (1.0f - e.alpha) * (float)nx / vv, c2 = 0.25f * (float)nx / vv;
-    float arg[NSG], sn[NSG];
-    const float spp = sh.tau[pp], cpp = sh.cmul[pp];
-#pragma unroll
-    for (int c = 0; c < NSG; ++c) {
-      arg[c] = 0.f;
-      if (c < e.nodes) {
-        const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
-                          sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
-        arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+  // ---------------- phase 2: u, grad u (or the SDGD Hessian diagonal) at (s, X_s) and f -> bsh
+  auto integrand = [&]() {
+    if constexpr (!GBM) {
+      float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
+      if (!ZERO && INTG) {
+        if constexpr (SPLIT)
+          mlp_tile_split<KIND, H, L>(e, net, sh, u, gs, gA, gB);
+        else
+          mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
       }
-      sn[c] = __sinf(arg[c]);
+      const int pp = 16 * wv + (lane & 15);
+      if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
+    } else {
+      // ffi (equations.py:457-466) with u_ii from SDGD (data.py:1273-1303); the baseline f_b
+      // gathers the point's Hessian diagonal at this path's indices (data.py:1293-1302).
+      const int jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
+      float s1 = 0.f, s2 = 0.f;
+      if (!ZERO && INTG) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+      const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
+      const float c1 = 0.5f * (1.0f - e.alpha) * (float)nx / vv, c2 = 0.25f * (float)nx / vv;
+      float arg[NSG], sn[NSG];
+      const float spp = sh.tau[pp], cpp = sh.cmul[pp];
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        arg[c] = 0.f;
+        if (c < e.nodes) {
+          const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
+                            sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
+          arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+        }
+        sn[c] = __sinf(arg[c]);
+      }
+      const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
+      float b1 = 0.f, b2 = 0.f;  // baseline Hessian diagonal gathered at this path's indices
+      for (int d = qq; d < nx; d += 4) {
+        const float c = (float)sh.cnt[d * P + pp], h = sh.hb[d];
+        b1 = fmaf(c, h, b1);
+        b2 = fmaf(c, fabsf(h), b2);
+      }
+      b1 = qsum(b1);
+      b2 = qsum(b2);
+      const float f = c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+      const float fbp = f_b + c1 * b1 + c2 * b2;
+      if (qq == 0) {
+        sh.bsh[pp] = INTG ? tmt * (f - fbp) : 0.f;
+        sh.fbp[pp] = fbp;
+      }
     }
-    const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
-    float b1 = 0.f, b2 = 0.f;  // baseline Hessian diagonal gathered at this path's indices
-    for (int d = qq; d < nx; d += 4) {
-      const float c = (float)sh.cnt[d * P + pp], h = sh.hb[d];
-      b1 = fmaf(c, h, b1);
-      b2 = fmaf(c, fabsf(h), b2);
-    }
-    b1 = qsum(b1);
-    b2 = qsum(b2);
-    const float f = c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
-    const float fbp = f_b + c1 * b1 + c2 * b2;
-    if (qq == 0) {
-      sh.bsh[pp] = INTG ? tmt * (f - fbp) : 0.f;
-      sh.fbp[pp] = fbp;
-    }
+  };
+
+  // Phase order.  Two workgroups share a CU; if both run their MFMA phase at the same time the
+  // matrix pipe idles during the (longer) VALU rollouts.  Workgroups on the "terminal last"
+  // order run the MLP between the integral and the terminal rollout, so a co-resident pair in
+  // opposite orders overlaps one's MFMA phase with the other's VALU phase.  The results do not
+  // depend on the order (same counters, same per-lane arithmetic).
+  bool tlast = false;
+  if constexpr (SPLIT) {
+    tlast = true;  // measured faster, and the terminal sums are not live across the MLP (no spills)
+  } else if constexpr (!GBM) {
+    if (a.order == 1) tlast = (__builtin_amdgcn_s_getreg((3 << 11) | (16 << 6) | 4) & 1) != 0;  // HW_ID.TG_ID
+    else if (a.order == 2) tlast = (blockIdx.x & 1) != 0;
+    else if (a.order == 3) tlast = ((blockIdx.x >> 8) & 1) != 0;
+    else if (a.order == 4) tlast = true;
   }
-  __syncthreads();
+  float ap;
+  if (!tlast) {
+    terminal_rollout();
+    integral_rollout();
+    ap = terminal_finish();
+    integrand();
+    __syncthreads();
+  } else {
+    integral_rollout();
+    __syncthreads();
+    integrand();
+    terminal_rollout();
+    ap = terminal_finish();  // its barrier also publishes bsh
+  }
 
   // ---------------- phase 3: per-path contributions -> per-block partial slab
   const float bp = sh.bsh[lane];
@@ -974,6 +1227,28 @@ static int upload(dpi_problem_s* p, const std::vector<T>& v, const T** out) {
   p->dev.push_back(d);
   *out = reinterpret_cast<const T*>(d);
   return 0;
+}
+
+// Append an R x C (C % 32 == 0) matrix in the fp16-split fragment order of mlp_tile_split:
+// row r, chunk u, lane group q: 8 hi halves then 8 lo halves of columns 32u + 4q + (j & 3) + 16 (j >> 2).
+// Returns the offset (in 4-byte words) into `blob`.
+template <class F>
+static size_t pack_split(std::vector<float>& blob, int R, int C, F at) {
+  const size_t off = blob.size();
+  blob.resize(off + (size_t)R * C, 0.f);
+  _Float16* dst = reinterpret_cast<_Float16*>(blob.data() + off);
+  for (int r = 0; r < R; ++r)
+    for (int u = 0; u < C / 32; ++u)
+      for (int q = 0; q < 4; ++q) {
+        _Float16* g = dst + ((size_t)r * C + 32 * u + 8 * q) * 2;  // 16 halves = 8 words
+        for (int j = 0; j < 8; ++j) {
+          const float x = at(r, 32 * u + 4 * q + (j & 3) + 16 * (j >> 2));
+          const _Float16 h = (_Float16)x;
+          g[j] = h;
+          g[8 + j] = (_Float16)((x - (float)h) * 2048.0f);
+        }
+      }
+  return off;
 }
 
 extern "C" {
@@ -1146,6 +1421,20 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   const size_t owout = take(H);
   for (int h = 0; h < H; ++h) blob[owout + h] = cur[h];
   const float bout = cur[H];
+  // fp16-split copies for the split MFMA path (H % 32 == 0)
+  const int nxp32 = (nx + 31) & ~31;
+  size_t oW1xS = 0, oW1xTS = 0, oWS[4] = {0}, oWTS[4] = {0};
+  if (H % 32 == 0) {
+    auto Wx = [&](int h, int d) { return d < nx ? W0[(size_t)h * n_in + 1 + d] : 0.f; };
+    oW1xS = pack_split(blob, H, nxp32, Wx);
+    oW1xTS = pack_split(blob, nxp32, H, [&](int d, int h) { return Wx(h, d); });
+    for (int l = 1; l < L; ++l) {
+      const float* Wl = blob.data() + oW[l];
+      std::vector<float> Wc(Wl, Wl + (size_t)H * H);
+      oWS[l] = pack_split(blob, H, H, [&](int r, int c) { return Wc[(size_t)r * H + c]; });
+      oWTS[l] = pack_split(blob, H, H, [&](int r, int c) { return Wc[(size_t)c * H + r]; });
+    }
+  }
   auto* n = new dpi_net_s();
   std::memset(&n->d, 0, sizeof(n->d));
   void* d = nullptr;
@@ -1177,6 +1466,16 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   }
   n->d.wout = base + owout;
   n->d.bout = bout;
+  n->d.nxp32 = nxp32;
+  if (H % 32 == 0) {
+    auto u32 = [&](size_t off) { return reinterpret_cast<const uint32_t*>(base + off); };
+    n->d.W1xS = u32(oW1xS);
+    n->d.W1xTS = u32(oW1xTS);
+    for (int l = 1; l < L; ++l) {
+      n->d.WS[l] = u32(oWS[l]);
+      n->d.WTS[l] = u32(oWTS[l]);
+    }
+  }
   *out = n;
   return 0;
 }
@@ -1407,17 +1706,22 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
 
 // GEMM precision: exact-fp32 MFMA by default; DPI_GEMM=f16x3 selects the fp16-split kernel
 // (same speed today: both are load-latency bound).
-static int g_gemm_mode = -1;  // -1: from the environment, 0: fp32, 1: fp16-split
-static bool gemm_f32() {
+static int g_gemm_mode = -1;  // -1: from the environment; DPI_GEMM_* of include/dpi.h
+static int gemm_mode() {
   if (g_gemm_mode < 0) {
     const char* e = std::getenv("DPI_GEMM");
-    g_gemm_mode = (e && std::strcmp(e, "f16x3") == 0) ? 1 : 0;
+    g_gemm_mode = !e ? DPI_GEMM_AUTO : std::strcmp(e, "f16x3") == 0 ? DPI_GEMM_F16X3
+                                   : std::strcmp(e, "f32") == 0   ? DPI_GEMM_F32
+                                                                  : DPI_GEMM_AUTO;
   }
-  return g_gemm_mode == 0;
+  return g_gemm_mode;
 }
+static bool gemm_f32() { return gemm_mode() != DPI_GEMM_F16X3; }  // PISGradNet GEMM pipeline
+static bool mlp_split() { return gemm_mode() != DPI_GEMM_F32; }   // fused MLP of k_paths
 
 extern "C" int dpi_set_gemm_precision(int mode) {
-  if (mode != 0 && mode != 1) return fail(DPI_ERR_ARG, "gemm precision: 0 = fp32, 1 = fp16-split");
+  if (mode != DPI_GEMM_F32 && mode != DPI_GEMM_F16X3 && mode != DPI_GEMM_AUTO)
+    return fail(DPI_ERR_ARG, "gemm precision: 0 = fp32, 1 = fp16-split, 2 = auto");
   g_gemm_mode = mode;
   return 0;
 }
@@ -1534,8 +1838,13 @@ static void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch
   if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTH), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                        q.bx, q.hb);
-  else
-    hipLaunchKernelGGL((k_paths<KIND, H, L, Z>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+  else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+    if (q.a->split)
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+    else
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+  } else
+    hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
 }
 
 template <int KIND>
@@ -1663,6 +1972,12 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   return 0;
 }
 
+// k_paths phase order policy (see the kernel); DPI_ORDER overrides for ablations.
+static int path_order() {
+  const char* e = std::getenv("DPI_ORDER");
+  return e ? std::atoi(e) : 0;
+}
+
 static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                         uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                         void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
@@ -1698,6 +2013,8 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.c3i = DPI_TAG_INT | (epoch << 8);
   a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.point_base = point_base;
+  a.order = path_order();
+  a.split = mlp_split() ? 1 : 0;
   hipStream_t st = (hipStream_t)stream;
   if (net->d.kind == 2) {
     if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st))) return rc;

@@ -75,7 +75,8 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
   float* row = rows + r * L.stride;
   const float U = u01_oc(philox4x32_10(0u, m, ig, c3s, k0, k1).x);
   const float s = fmaf(U, tmt, t);
-  const float cI = e.asq * sqrtf((s - t) / Kf);
+  const float smt = U * tmt;  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
+  const float cI = e.asq * sqrtf(smt / Kf);
   const float cT = e.asq * sqrtf(tmt / Kf);
   __syncthreads();
   float gst[NSG];
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
     row[L.SC + 0] = s;
     row[L.SC + 1] = cI;
     row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
-    row[L.SC + 3] = 0.f;
+    row[L.SC + 3] = smt;
   }
 }
 
@@ -248,11 +249,11 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   const float f_b = fbv[i];
   const int p = tid >> 2, q = tid & 3;
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;
-  const float s = row[L.SC + 0], ap = row[L.SC + 2];
+  const float s = row[L.SC + 0], ap = row[L.SC + 2], smt = row[L.SC + 3];
   float A, B, sm;
   pis_z_stats(e, pn, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
-  const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * (s - t)) * e.asq);
+  const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * smt) * e.asq);
   if (q == 0) {
     const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
     cs[0][p][0] = c0;

@@ -106,8 +106,15 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
                            size_t n_params, dpi_net* out);
 int dpi_net_destroy(dpi_net net);
 
-/* MFMA precision of the layer-wise GEMM pipeline (PISGradNet): 0 = exact fp32 (default),
- * 1 = fp16-split x = hi + 2^-11 lo, three f16 MFMAs per product (~2.4e-7 relative error). */
+/* MFMA precision of the network evaluations.  DPI_GEMM_F32: v_mfma_f32_16x16x4_f32 everywhere.
+ * DPI_GEMM_F16X3: fp16-split x = hi + 2^-11 lo, three v_mfma_f32_16x16x32_f16 per product
+ * (~2.4e-7 relative error, same tolerance class as fp32) everywhere.  DPI_GEMM_AUTO (default):
+ * fp16-split for the fused MLP of the path kernel (hidden width % 32 == 0), fp32 for the
+ * PISGradNet GEMM pipeline.  The environment variable DPI_GEMM=f32|f16x3 sets the initial mode.
+ * Replaces no reference interface (the reference evaluates u in torch fp64/fp32). */
+#define DPI_GEMM_F32 0
+#define DPI_GEMM_F16X3 1
+#define DPI_GEMM_AUTO 2
 int dpi_set_gemm_precision(int mode);
 
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */

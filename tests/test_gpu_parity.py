@@ -86,7 +86,17 @@ def _oracle_mlp(m):
                  ["ELU"] * (len(lin) - 1))
 
 
-def test_burgers_full_network_K50_vs_oracle():
+@pytest.fixture(params=["f32", "auto"])
+def mlp_precision(request):
+    """Fused-MLP MFMA precision: exact fp32 or the default fp16-split (include/dpi.h DPI_GEMM_*)."""
+    from deeppicarditeration_amd import _lib as L
+    mode = L.DPI_GEMM_F32 if request.param == "f32" else L.DPI_GEMM_AUTO
+    L.check(L.load().dpi_set_gemm_precision(mode), "gemm precision")
+    yield request.param
+    L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "gemm precision")
+
+
+def test_burgers_full_network_K50_vs_oracle(mlp_precision):
     """Config-2 network (4x128 ELU) and K = 50 at a size the fp64 oracle finishes quickly."""
     import deeppicarditeration_amd as dpi
     eq = dpi.Cha(100, 1.0, 5.0, 1.0)
@@ -97,10 +107,32 @@ def test_burgers_full_network_K50_vs_oracle():
     oeq = O.Cha(100, 1.0, 5.0, 1.0)
     ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 512, 50, 1, 0, 0)
     parts = rel_l2_parts(y.cpu().numpy(), ref)
+    print("mlp precision", mlp_precision, parts)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-def test_hjb_ou_mlp_vs_oracle():
+@pytest.mark.parametrize("net_kind", ["zero", "mlp"])
+def test_tiny_s_minus_t_regression(net_kind):
+    """Point 520 of (seed 0, epoch 1) has a path with U = O(2^-24) at t = 0.933: fp32 s - t rounds
+    to 0 there, which once turned Y_s into inf and the gradient labels into -inf / NaN.  The
+    kernels use s - t = U (T - t); the label must be finite and match the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.Cha(8, 1.0, 5.0, 1.0)
+    net = dpi.ZeroSolution(1) if net_kind == "zero" else _random_mlp(eq, [32, 32], 5)
+    gen = dpi.OnlineDataGenerator(eq, net, 3, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=1024,
+                                  n_estimate_integral=1024, n_euler_steps=4, seed=0, epoch=1)
+    tx, pb = gen.sample_t_and_x(1, point_base=520)
+    assert abs(float(tx[0, 0]) - 0.9333475) < 1e-6
+    y = gen.generate_with_gradients(tx, point_base=pb)
+    assert torch.isfinite(y).all()
+    oeq = O.Cha(8, 1.0, 5.0, 1.0)
+    onet = O.ZeroNet() if net_kind == "zero" else _oracle_mlp(net)
+    ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 1024, 4, 0, 1, 520)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_hjb_ou_mlp_vs_oracle(mlp_precision):
     import deeppicarditeration_amd as dpi
     eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
                                alpha_scale=4.0)
@@ -148,7 +180,7 @@ def test_hjb_pisgradnet_config3_network_vs_oracle(gemm_mode):
     oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
     onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
     ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 20, 2, 1, 0)
-    L.check(L.load().dpi_set_gemm_precision(0), "gemm precision")
+    L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "gemm precision")
     parts = rel_l2_parts(y.cpu().numpy(), ref)
     print("gemm mode", gemm_mode, parts)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
