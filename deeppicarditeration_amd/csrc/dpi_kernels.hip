@@ -79,11 +79,51 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// gfx950 cross-half / cross-row lane swaps (VALU, no LDS): for the pair (a, b) the two results
+// sum to [a_lo + a_hi | b_lo + b_hi] (halves of 32 lanes) resp. the same over rows of 16 lanes.
+__device__ __forceinline__ float swap32_sum(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_sum(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 // sum over the 4 lane groups (lanes j, j+16, j+32, j+48) of the MFMA C layout
 __device__ __forceinline__ float qsum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+  v = swap32_sum(v, v);
+  return swap16_sum(v, v);
+}
+// Column sums of a 64 x 64 block: v[c] is lane l's value of column c; on return lane l holds the
+// sum over all 64 lanes of column l.  A halving butterfly: at level m = 32, 16, ..., 1 a lane
+// keeps the lower half of its columns if (lane & m) == 0, else the upper half, and adds its
+// partner's copy of the kept half — 63 exchanges for 64 columns instead of 6 per column.  The
+// summation order of every column is fixed (independent of which block or rank runs it).
+template <int M>
+__device__ __forceinline__ float dpp_take(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), M, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float column_sums64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = swap32_sum(v[j], v[j + 32]);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = swap16_sum(v[j], v[j + 16]);
+  // within rows of 16: partners by row_mirror (i <-> 15 - i), row_half_mirror (i <-> 7 - i),
+  // quad_perm [2,3,0,1] and [1,0,3,2]; the side is the lane bit m in every case
+#define DPI_BFLY(MASK, H, CTRL)                                  \
+  _Pragma("unroll") for (int j = 0; j < H; ++j) {                \
+    const bool up = (lane & MASK) != 0;                          \
+    const float keep = up ? v[j + H] : v[j];                     \
+    const float send = up ? v[j] : v[j + H];                     \
+    v[j] = keep + dpp_take<CTRL>(send);                          \
+  }
+  DPI_BFLY(8, 8, 0x140)
+  DPI_BFLY(4, 4, 0x141)
+  DPI_BFLY(2, 2, 0x4E)
+  DPI_BFLY(1, 1, 0xB1)
+#undef DPI_BFLY
+  return v[0];
 }
 
 // Stage rows [r0, r0 + nrows) of a row-major global matrix with ncol floats per row
@@ -124,26 +164,20 @@ __device__ __forceinline__ void split_act(const float (&t0)[4], const float (&t1
   const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
   split8(x, hi, lo);
 }
-// Stage rows [r0, r0 + nrows) of a split-packed matrix (C words per row) into LDS rows of C + 4
-// words (C + 4 = 4 mod 64 or 36 mod 64 words: the 16 rows of a ds_read_b128 hit distinct banks).
-__device__ __forceinline__ void stage_rows_split(const uint32_t* __restrict__ g, int C, int r0, int nrows,
-                                                 uint32_t* wsh) {
-  const int n4 = C >> 2, st = C + 4;
-  for (int idx = threadIdx.x; idx < nrows * n4; idx += NTH) {
-    const int r = idx / n4, c = idx - r * n4;
-    const u32v4 v = *reinterpret_cast<const u32v4*>(g + (size_t)(r0 + r) * C + 4 * c);
-    *reinterpret_cast<u32v4*>(wsh + r * st + 4 * c) = v;
-  }
-}
-__device__ __forceinline__ void load_a_split(const uint32_t* wsh, int st, int row, int u, int q, half8& ah,
+// Split chunks sit in LDS unpadded (C words per row, as LDS-DMA writes 1 KiB lane-linear per wave
+// instruction) with the 16-B granules of row r XOR-swizzled: granule g is stored at g ^ (r & m),
+// m = min(15, C/4 - 1).  The 16 lanes of each ds_read_b128 lane group then hit distinct banks.
+__device__ __forceinline__ int split_swz(int C) { return C >= 64 ? 15 : (C >> 2) - 1; }
+__device__ __forceinline__ void load_a_split(const uint32_t* wsh, int C, int row, int u, int q, half8& ah,
                                              half8& al) {
-  const uint32_t* p = wsh + row * st + u * 32 + q * 8;
-  ah = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(p));
-  al = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(p + 4));
+  const int m = split_swz(C), g = 8 * u + 2 * q, x = row & m;
+  const uint32_t* rp = wsh + row * C;
+  ah = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp + 4 * (g ^ x)));
+  al = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp + 4 * ((g + 1) ^ x)));
 }
 // 32 output rows (tiles T0, T0+1) of W B for a staged 32-row chunk; B pre-split per chunk u.
 template <int NU>
-__device__ __forceinline__ void split_rows32(const uint32_t* wsh, int st, int jj, int qq, const half8 (&bh)[NU],
+__device__ __forceinline__ void split_rows32(const uint32_t* wsh, int C, int jj, int qq, const half8 (&bh)[NU],
                                              const half8 (&bl)[NU], floatx4 (&out)[2]) {
   floatx4 am[2], ac[2];
 #pragma unroll
@@ -153,7 +187,7 @@ __device__ __forceinline__ void split_rows32(const uint32_t* wsh, int st, int jj
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       half8 ah, al;
-      load_a_split(wsh, st, 16 * t + jj, u, qq, ah, al);
+      load_a_split(wsh, C, 16 * t + jj, u, qq, ah, al);
       am[t] = mfma16(ah, bh[u], am[t]);
       ac[t] = mfma16(ah, bl[u], ac[t]);
       ac[t] = mfma16(al, bh[u], ac[t]);
@@ -172,8 +206,8 @@ namespace dpi {
 // LDS layout (floats) shared by the baseline and path kernels.
 struct Lds {
   float S[NXP_MAX * SS];   // [dim][path] integral noise sums (path kernel) / x tile (baseline)
-  float W[32 * WST];       // weight chunk
-  float vec[6 * HMAX];     // base0 | w1t | b1(layer bias l) ... | wout | c1
+  float W[2 * 32 * HMAX];  // weight chunk: f32 rows of stride WST, or two split chunks (LDS-DMA ring)
+  float vec[4 * HMAX];     // base0 | w1t | wout | c1
   float bh[4 * HMAX];      // hidden-layer biases
   float xsh[NXP_MAX];      // point x (path kernel) / zeros (baseline)
   float gst[4 * P * NSG];  // per-wave partial g statistics
@@ -349,6 +383,68 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
   }
 }
 
+// Weight-chunk stream of the split MLP: every 32-row chunk of every matrix, in use order, is
+// copied global -> LDS by LDS-DMA one chunk ahead into a two-slot ring (the copy overlaps the
+// MFMAs of the current chunk; no registers, one barrier per chunk).
+// Chunk index -> (matrix, C, row offset): layer 1 (W1x), hidden layers (W_l), backward
+// (W_{l+1}^T, l = L-2..0), then — GRAD_FULL only — the input gradient (W1x^T).
+template <int H, int L>
+struct SplitStream {
+  static constexpr int NT = H / 32;  // chunks per H-row matrix
+  const NetDev& net;
+  int C1, n1, nT1, total;
+  __device__ SplitStream(const NetDev& n, bool grad_full) : net(n) {
+    C1 = n.nxp32;
+    n1 = NT;                               // layer-1 chunks (H output rows)
+    nT1 = C1 / 32;                         // W1x^T chunks (C1 output rows)
+    total = n1 + 2 * (L - 1) * NT + (grad_full ? nT1 : 0);
+  }
+  __device__ __forceinline__ void desc(int idx, const uint32_t*& g, int& C, int& r0) const {
+    if (idx < n1) {
+      g = net.W1xS, C = C1, r0 = 32 * idx;
+      return;
+    }
+    idx -= n1;
+    if (idx < (L - 1) * NT) {
+      g = net.WS[1 + idx / NT], C = H, r0 = 32 * (idx % NT);
+      return;
+    }
+    idx -= (L - 1) * NT;
+    if (idx < (L - 1) * NT) {
+      g = net.WTS[L - 1 - idx / NT], C = H, r0 = 32 * (idx % NT);
+      return;
+    }
+    idx -= (L - 1) * NT;
+    g = net.W1xTS, C = H, r0 = 32 * idx;
+  }
+  // LDS-DMA of chunk idx into ring slot idx & 1: wave-instruction w writes LDS granules
+  // [64 w, 64 w + 64) lane-linearly; lane i's source is the granule that belongs there.
+  __device__ __forceinline__ void issue(int idx, uint32_t* ring) const {
+    if (idx >= total) return;
+    const uint32_t* g;
+    int C, r0;
+    desc(idx, g, C, r0);
+    uint32_t* dst = ring + (idx & 1) * (32 * HMAX);
+    const int gpr = C >> 2, m = split_swz(C), lane = threadIdx.x & 63;
+    for (int w = threadIdx.x >> 6; w < (C >> 3); w += NTH / 64) {
+      const int G = 64 * w + lane, r = G / gpr, gs = (G - r * gpr) ^ (r & m);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(g + (size_t)(r0 + r) * C + 4 * gs),
+          (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+    }
+  }
+  // One barrier per chunk: it retires this wave's DMA of chunk idx (vmcnt(0) before s_barrier)
+  // and every wave's reads of chunk idx - 1, whose slot then receives chunk idx + 1.
+  __device__ __forceinline__ const uint32_t* enter(int idx, uint32_t* ring, int& C) const {
+    const uint32_t* g;
+    int r0;
+    desc(idx, g, C, r0);
+    __syncthreads();
+    issue(idx + 1, ring);
+    return ring + (idx & 1) * (32 * HMAX);
+  }
+};
+
 // mlp_tile on the fp16-split MFMA (H % 32 == 0): same inputs, outputs and tile layout; each
 // 16x16x4 f32 chain becomes 16x16x32 f16 chunks (3 MFMAs per 32-wide chunk instead of 8), the
 // weights come pre-split from NetDev::*S, the activations are split in registers.
@@ -363,32 +459,40 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   const float tau = sh.tau[pp];
   const float cm = sh.cmul[pp];
   uint32_t* wsh = reinterpret_cast<uint32_t*>(sh.W);
-  const int C1 = net.nxp32, nu1 = C1 >> 5;
+  SplitStream<H, L> ss(net, Eq<KIND>::GRAD_FULL);
+  const int nu1 = ss.C1 >> 5;
+  int chunk = 0;
+  ss.issue(0, wsh);
   float act[L][HT][4];
   half8 bh[NU], bl[NU];
 
   // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+  half8 xh[NXP_MAX / 32], xl[NXP_MAX / 32];  // the noise tile as B operand, split once
+#pragma unroll
+  for (int u = 0; u < NXP_MAX / 32; ++u) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = u < nu1 ? sh.S[(32 * u + 4 * qq + (j & 3) + 16 * (j >> 2)) * SS + pp] : 0.f;
+    split8(x, xh[u], xl[u]);
+  }
 #pragma unroll
   for (int T0 = 0; T0 < HT; T0 += 2) {
-    __syncthreads();
-    stage_rows_split(net.W1xS, C1, 16 * T0, 32, wsh);
-    __syncthreads();
+    int C;
+    const uint32_t* wch = ss.enter(chunk++, wsh, C);
     floatx4 am[2], ac[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int u = 0; u < nu1; ++u) {
-      float x[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = sh.S[(32 * u + 4 * qq + (j & 3) + 16 * (j >> 2)) * SS + pp];
-      half8 xh, xl;
-      split8(x, xh, xl);
+    for (int u = 0; u < NXP_MAX / 32; ++u) {
+      if (u < nu1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        half8 ah, al;
-        load_a_split(wsh, C1 + 4, 16 * t + jj, u, qq, ah, al);
-        am[t] = mfma16(ah, xh, am[t]);
-        ac[t] = mfma16(ah, xl, ac[t]);
-        ac[t] = mfma16(al, xh, ac[t]);
+        for (int t = 0; t < 2; ++t) {
+          half8 ah, al;
+          load_a_split(wch, C, 16 * t + jj, u, qq, ah, al);
+          am[t] = mfma16(ah, xh[u], am[t]);
+          ac[t] = mfma16(ah, xl[u], ac[t]);
+          ac[t] = mfma16(al, xh[u], ac[t]);
+        }
       }
     }
 #pragma unroll
@@ -407,11 +511,10 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
     for (int u = 0; u < NU; ++u) split_act(act[l - 1][2 * u], act[l - 1][2 * u + 1], bh[u], bl[u]);
 #pragma unroll
     for (int T0 = 0; T0 < HT; T0 += 2) {
-      __syncthreads();
-      stage_rows_split(net.WS[l], H, 16 * T0, 32, wsh);
-      __syncthreads();
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
       floatx4 o[2];
-      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -437,11 +540,10 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
     for (int u = 0; u < NU; ++u) split_act(act[l + 1][2 * u], act[l + 1][2 * u + 1], bh[u], bl[u]);
 #pragma unroll
     for (int T0 = 0; T0 < HT; T0 += 2) {
-      __syncthreads();
-      stage_rows_split(net.WTS[l + 1], H, 16 * T0, 32, wsh);
-      __syncthreads();
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
       floatx4 o[2];
-      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -461,12 +563,11 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
 #pragma unroll
     for (int u = 0; u < NU; ++u) split_act(act[0][2 * u], act[0][2 * u + 1], bh[u], bl[u]);
     float A = 0.f, B = 0.f;
-    for (int T0 = 0; T0 < (C1 >> 4); T0 += 2) {
-      __syncthreads();
-      stage_rows_split(net.W1xTS, H, 16 * T0, 32, wsh);
-      __syncthreads();
+    for (int T0 = 0; T0 < (ss.C1 >> 4); T0 += 2) {
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
       floatx4 o[2];
-      split_rows32<NU>(wsh, H + 4, jj, qq, bh, bl, o);
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -1087,6 +1188,25 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   // partial slab layout [point][2F][block]: the reduce kernel reads each column's blocks contiguously
   float* out = a.partial + (size_t)i * 2 * F * a.nbp + blk;
   const int nbs = a.nbp;
+  // per-block sums of c and c^2 for this wave's columns: 2 per owned dim (d = 4 (wv + 4c) + q,
+  // column 8c + 2q + {0: sum, 1: sum of squares}) and, on wave 0, the value column (56, 57)
+  const float aY = ap * yT, bY = bp * yI;
+  float col[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) col[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const int j = wv + 4 * c;
+    if (j < nb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        const float v = d < nx ? fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]) : 0.f;
+        col[8 * c + 2 * q] = v;
+        col[8 * c + 2 * q + 1] = v * v;
+      }
+    }
+  }
   if (wv == 0) {
     float fbt;
     if constexpr (GBM)
@@ -1094,27 +1214,29 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
     else
       fbt = f_b + Eq<KIND>::ffc(e);
     const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
-    const float s1 = wave_sum(c0), s2 = wave_sum(c0 * c0);
-    if (lane == 0) {
-      out[0] = s1;
-      out[(size_t)F * nbs] = s2;
+    col[56] = c0;
+    col[57] = c0 * c0;
+  }
+  const float tot = column_sums64(col);
+  {
+    const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
+    const int d = 4 * (wv + 4 * c) + q;
+    if (lane < 56) {
+      if (wv + 4 * c < nb && d < nx) out[(size_t)(sq * F + 1 + d) * nbs] = tot;
+    } else if (wv == 0 && lane < 58) {
+      out[(size_t)(sq * F) * nbs] = tot;
     }
   }
-  const float aY = ap * yT, bY = bp * yI;
+  if (wv + 28 < nb) {  // nx > 112: the eighth dim-block of this wave, one column at a time
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int j = wv + 4 * c;
-    if (j < nb) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * j + q;
-        if (d < nx) {
-          const float v = fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]);
-          const float s1 = wave_sum(v), s2 = wave_sum(v * v);
-          if (lane == 0) {
-            out[(size_t)(1 + d) * nbs] = s1;
-            out[(size_t)(F + 1 + d) * nbs] = s2;
-          }
+    for (int q = 0; q < 4; ++q) {
+      const int d = 4 * (wv + 28) + q;
+      if (d < nx) {
+        const float v = fmaf(aY, ST[7][q], bY * sh.S[d * SS + lane]);
+        const float s1 = wave_sum(v), s2 = wave_sum(v * v);
+        if (lane == 0) {
+          out[(size_t)(1 + d) * nbs] = s1;
+          out[(size_t)(F + 1 + d) * nbs] = s2;
         }
       }
     }

@@ -132,6 +132,22 @@ def test_tiny_s_minus_t_regression(net_kind):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
+@pytest.mark.parametrize("nx", [1, 7, 113, 128])
+def test_dimension_edges_vs_oracle(nx, mlp_precision):
+    """Ragged and maximal state dimensions: a partial last 4-dim block (7, 113), the 8th block of
+    a wave (nx > 112 takes the per-column reduction path) and nx = NXP_MAX = 128."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.Cha(nx, 1.0, 5.0, 1.0)
+    net = _random_mlp(eq, [64, 64], 11)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=3, seed=4, epoch=3)
+    tx, y = gen.sample_with_gradients(3)
+    oeq = O.Cha(nx, 1.0, 5.0, 1.0)
+    ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 128, 3, 4, 3, 0)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
 def test_hjb_ou_mlp_vs_oracle(mlp_precision):
     import deeppicarditeration_amd as dpi
     eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
