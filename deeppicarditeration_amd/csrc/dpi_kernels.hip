@@ -774,33 +774,57 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+constexpr int NTHB = 1024;  // baseline workgroup: 16 waves
+__device__ __forceinline__ float block_sum_b(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float a = 0.f;
+  for (int w = 0; w < NTHB / 64; ++w) a += red[w];
+  return a;
+}
+
 // Baseline per point (one workgroup per point): g(x), the state-dependent part of
 // f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
-// f_baseline).  A latency-bound handful of points, so one thread per hidden unit computes its
-// fp32 dot product (weights read coalesced through the transposed copies), no LDS staging.
+// f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
+// over k-slices (weights read coalesced through the transposed copies), no LDS staging.
 template <int KIND, bool ZERO>
-__global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
+__global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
                                                   float* __restrict__ gx, float* __restrict__ fb,
                                                   float* __restrict__ bx, float* __restrict__ hb) {
   __shared__ float xs[NXP_MAX];
   __shared__ float act[4][HMAX];
   __shared__ float dbuf[2][HMAX];
-  __shared__ float red[8];
+  __shared__ float red[NTHB / 64];
   const int i = blockIdx.x, tid = threadIdx.x;
   const int nx = e.nx, F = 1 + nx;
   const float* row = tx + (size_t)i * F;
   const float t = row[0];
-  for (int d = tid; d < NXP_MAX; d += NTH) xs[d] = d < nx ? row[1 + d] : 0.f;
+  for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
   __syncthreads();
-  // g(x): per-thread dims, then per-statistic block sums in fixed order
+  // g(x): per-thread dims, then per-statistic block sums in fixed order (one barrier pair)
   {
+    __shared__ float redn[NTHB / 64][NSG];
     float st[NSG];
 #pragma unroll
     for (int c = 0; c < NSG; ++c) st[c] = 0.f;
-    for (int d = tid; d < nx; d += NTH) Eq<KIND>::gstat(e, d, xs[d], st);
+    for (int d = tid; d < nx; d += NTHB) Eq<KIND>::gstat(e, d, xs[d], st);
 #pragma unroll
-    for (int c = 0; c < NSG; ++c) st[c] = block_sum(st[c], red);
-    if (tid == 0) gx[i] = Eq<KIND>::gfin(e, st);
+    for (int c = 0; c < NSG; ++c) st[c] = wave_sum(st[c]);
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) redn[tid >> 6][c] = st[c];
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float a = 0.f;
+        for (int w = 0; w < NTHB / 64; ++w) a += redn[w][c];
+        st[c] = a;
+      }
+      gx[i] = Eq<KIND>::gfin(e, st);
+    }
   }
   float Cb = 0.f;
   if constexpr (KIND == DPI_EQ_GBM) {
@@ -810,15 +834,15 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
     for (int c = 0; c < NSG; ++c) {
       float v = 0.f;
       if (c < e.nodes)
-        for (int d = tid; d < nx; d += NTH) v = fmaf(e.gw[c * F + 1 + d], xs[d], v);
-      v = block_sum(v, red);
+        for (int d = tid; d < nx; d += NTHB) v = fmaf(e.gw[c * F + 1 + d], xs[d], v);
+      v = block_sum_b(v, red);
       arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, v) : 0.f;
       sn[c] = __sinf(arg[c]);
     }
-    const float ah = block_sum(Eq<KIND>::abs_hess_partial(e, sn, tid, NTH), red);
+    const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
     Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
     if (ZERO) {
-      for (int d = tid; d < NXP_MAX; d += NTH) hb[(size_t)i * NXP_MAX + d] = 0.f;
+      for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
       if (tid == 0) fb[i] = Cb;
       return;
     }
@@ -828,21 +852,42 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
     return;
   }
   const int H = net.H, L = net.L, nxp = net.nxp;
-  // layer 1
-  if (tid < H) {
-    float acc = 0.f;
-    for (int d = 0; d < nx; ++d) acc = fmaf(net.W1xT[(size_t)d * H + tid], xs[d], acc);
-    bx[(size_t)i * H + tid] = net.b1[tid] + acc;
-    act[0][tid] = elu(fmaf(net.w1t[tid], t, net.b1[tid] + acc));
-  }
-  __syncthreads();
-  for (int l = 1; l < L; ++l) {
-    if (tid < H) {
-      float acc = net.b[l][tid];
-      const float* wt = net.WT[l];
-      for (int k = 0; k < H; ++k) acc = fmaf(wt[(size_t)k * H + tid], act[l - 1][k], acc);
-      act[l][tid] = elu(acc);
+  // Mat-vecs y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), coalesced in h): thread tid takes
+  // unit h = tid % H and the k-slice tid / H of NTHB / H slices (<= 16 values, all loads issued
+  // before the first FMA: one memory latency per layer); the slices are added in fixed order by
+  // the unit's owner.
+  __shared__ float part[NTHB];
+  auto matvec = [&](const float* __restrict__ Wt, const float* v, int K) -> float {
+    const int h = tid % H, ns = NTHB / H, sl = tid / H;
+    const int kc = (K + ns - 1) / ns, k0 = sl * kc, k1 = min(K, k0 + kc);  // kc <= 16
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = k0 + j < k1 ? Wt[(size_t)(k0 + j) * H + h] : 0.f;  // all loads in flight
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      if (k0 + j < k1) a0 = fmaf(w[j], v[k0 + j], a0);
+      if (k0 + j + 1 < k1) a1 = fmaf(w[j + 1], v[k0 + j + 1], a1);
     }
+    part[tid] = a0 + a1;
+    __syncthreads();
+    float y = 0.f;
+    if (tid < H)
+      for (int j = 0; j < ns; ++j) y += part[j * H + tid];
+    return y;  // valid for tid < H; the caller's barrier precedes the next use of part
+  };
+  // layer 1
+  {
+    const float acc = matvec(net.W1xT, xs, nx);
+    if (tid < H) {
+      bx[(size_t)i * H + tid] = net.b1[tid] + acc;
+      act[0][tid] = elu(fmaf(net.w1t[tid], t, net.b1[tid] + acc));
+    }
+    __syncthreads();
+  }
+  for (int l = 1; l < L; ++l) {
+    const float acc = matvec(net.WT[l], act[l - 1], H);
+    if (tid < H) act[l][tid] = elu(acc + net.b[l][tid]);
     __syncthreads();
   }
   if constexpr (KIND == DPI_EQ_GBM) {
@@ -861,7 +906,7 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
       }
       __syncthreads();
     }
-    for (int d = tid; d < nx; d += NTH) {
+    for (int d = tid; d < nx; d += NTHB) {
       float ud = 0.f;
       for (int h = 0; h < H; ++h) {
         const float z = net.W1x[(size_t)h * nxp + d];
@@ -884,32 +929,29 @@ __global__ __launch_bounds__(256) void k_baseline(EqDev e, NetDev net, const flo
     if (tid == 0) fb[i] = Cb;
     return;
   }
-  const float u = block_sum(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
+  const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
   int cur = 0;
   if (tid < H) dbuf[0][tid] = net.wout[tid] * delu_from_a(act[L - 1][tid]);
   __syncthreads();
   for (int l = L - 2; l >= 0; --l) {
-    if (tid < H) {
-      const float* w = net.W[l + 1];  // (H_out, H_in) row-major: column tid is coalesced across threads
-      float acc = 0.f;
-      for (int k = 0; k < H; ++k) acc = fmaf(w[(size_t)k * H + tid], dbuf[cur][k], acc);
-      dbuf[cur ^ 1][tid] = acc * delu_from_a(act[l][tid]);
-    }
+    // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
+    const float acc = matvec(net.W[l + 1], dbuf[cur], H);
+    if (tid < H) dbuf[cur ^ 1][tid] = acc * delu_from_a(act[l][tid]);
     cur ^= 1;
     __syncthreads();
   }
   float gs = 0.f, gA = 0.f, gB = 0.f;
   if (!Eq<KIND>::GRAD_FULL) {
-    gs = block_sum(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
+    gs = block_sum_b(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
   } else {
     float A = 0.f, B = 0.f;
-    for (int d = tid; d < nx; d += NTH) {
+    for (int d = tid; d < nx; d += NTHB) {
       float z = 0.f;
       for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], dbuf[cur][k], z);
       Eq<KIND>::gacc(e, d, xs[d], z, A, B);
     }
-    gA = block_sum(A, red);
-    gB = block_sum(B, red);
+    gA = block_sum_b(A, red);
+    gB = block_sum_b(B, red);
   }
   if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
 }
@@ -1958,7 +2000,7 @@ struct Launch {
 template <int KIND, int H, int L, bool Z>
 static void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if (q.baseline)
-    hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTH), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+    hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                        q.bx, q.hb);
   else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
     if (q.a->split)
@@ -2044,7 +2086,7 @@ static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, cons
   if (rc) return rc;
   float *gx = (float*)(b + w.gx), *fb = (float*)(b + w.fb), *rows = (float*)(b + w.rows);
   // g(x) (k_baseline's zero-net instance also writes a placeholder f_b, overwritten below)
-  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTH), 0, st, p->e, net->d, tx, n, gx, fb,
+  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTHB), 0, st, p->e, net->d, tx, n, gx, fb,
                      (float*)(b + w.bx), (float*)(b + w.hb));
   const int F = 1 + p->e.nx;
   const PisRows L = pis_rows_layout(net->pis);
