@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed steps for this long before the warmup")
     ap.add_argument("--cpu-sample-paths", type=int, default=512, help="MC paths per point in the CPU sample")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="burgers")
     return ap.parse_args()
@@ -73,9 +74,9 @@ def _make(wl, dpi):
     return eq, net
 
 
-def cpu_baseline(wl, sample_paths):
+def cpu_baseline(wl, sample_paths, target_s=10.0):
     """Time the CPU oracle (oracle/: numpy fp64 restatement) on a bounded sample of the same
-    workload: 1 point x `sample_paths` paths x K, same network."""
+    workload: whole points of `sample_paths` paths x K, same network, until ~target_s seconds."""
     from oracle import dpi_oracle as O
     import deeppicarditeration_amd as dpi
     eq, net = _make(wl, dpi)
@@ -91,14 +92,23 @@ def cpu_baseline(wl, sample_paths):
         lin = [l for l in net if isinstance(l, torch.nn.Linear)]
         onet = O.MLP([l.weight.detach().double().numpy() for l in lin], [l.bias.detach().double().numpy() for l in lin],
                      ["ELU"] * (len(lin) - 1))
-    tx = O.sample_points(oeq, 1, seed=1)
+    from threadpoolctl import threadpool_limits
+    done, pts = 0, 0
     t0 = time.perf_counter()
-    O.labels_grad(oeq, onet, tx, sample_paths, wl["K"], 1, 0, 0, v=wl["sdgd"], m_chunk=min(sample_paths, 256))
-    dt = time.perf_counter() - t0
-    cores = 1  # numpy elementwise Philox/Box–Muller runs on one thread
-    return {"value": sample_paths / dt, "unit": "path-labels/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/dpi_oracle.py labels_grad, fp64 numpy, 1 point x {sample_paths} paths x K={wl['K']}, "
-                      f"{dt:.1f} s on {platform.processor() or platform.machine()} (os.cpu_count={os.cpu_count()})"}
+    with threadpool_limits(limits=1):  # the restatement is a scalar port: one thread, BLAS included
+        while True:
+            tx = O.sample_points(oeq, 1, seed=1, point_base=pts)
+            O.labels_grad(oeq, onet, tx, sample_paths, wl["K"], 1, 0, pts, v=wl["sdgd"],
+                          m_chunk=min(sample_paths, 256))
+            done += sample_paths
+            pts += 1
+            dt = time.perf_counter() - t0
+            if dt >= target_s:
+                break
+    return {"value": done / dt, "unit": "path-labels/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/dpi_oracle.py labels_grad, fp64 numpy, 1 thread, {pts} point(s) x {sample_paths} "
+                      f"paths x K={wl['K']} of this workload, {dt:.1f} s on "
+                      f"{platform.processor() or platform.machine()} (os.cpu_count={os.cpu_count()})"}
 
 
 def main():
@@ -140,6 +150,22 @@ def main():
         ev.append((e0, e1))
         return y
 
+    # Clock ramp: the GPU needs ~10 ms of load to leave its idle clocks, which a 20-step run at
+    # ~0.4 ms/step would otherwise spend mostly in.  Run untimed steps for PREWARM_S seconds of
+    # wall time first (steady state is what a Picard run sees: it generates labels for minutes),
+    # then the W warmup steps of the contract.
+    prewarm = 0
+    t_pw = time.perf_counter()
+    while True:
+        for _ in range(16):
+            step()
+        prewarm += 16
+        torch.cuda.synchronize()
+        go = torch.tensor([1.0 if time.perf_counter() - t_pw < args.prewarm_s else 0.0], device=dev)
+        if dist:  # every rank runs the same number of steps (each step holds a collective)
+            dist.broadcast(go, src=0)
+        if go.item() == 0.0:
+            break
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -185,6 +211,7 @@ def main():
             "config": {"workload": wl["desc"], "baseline_config": wl["cfg"],
                        "points": N_POINTS, "mc_paths_per_gpu": M_PER_GPU, "euler_steps": K_STEPS, "nx": NX,
                        "parallelism": f"mc-shard{world}", "per_gpu_value": value / world,
+                       "prewarm_steps": prewarm,
                        "rel_l2_vs_ref": "<= 3e-7 measured, tolerance 1e-4 (tests/test_gpu_parity.py)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,

@@ -906,25 +906,39 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       }
       __syncthreads();
     }
-    for (int d = tid; d < nx; d += NTHB) {
-      float ud = 0.f;
-      for (int h = 0; h < H; ++h) {
-        const float z = net.W1x[(size_t)h * nxp + d];
-        ztb[0][h][d] = z;
-        ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
+    // Tangent sweep as an LDS mat-mat per layer: thread (d = tid % 128, hg = tid / 128) owns the
+    // rows h = hg, hg + 8, ... of the tangent Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k]) Z_{l-1}[k][d].
+    __shared__ float wsc[64 * 65];
+    __shared__ float udp[8][NXP_MAX];
+    const int d = tid % NXP_MAX, hg = tid / NXP_MAX;  // NTHB = 8 x NXP_MAX
+    float ud = 0.f;
+    for (int h = hg; h < H; h += 8) {
+      const float z = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
+      ztb[0][h][d] = z;
+      ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
+    }
+    int cz = 0;
+    for (int l = 1; l < L; ++l) {
+      for (int q = tid; q < H * H; q += NTHB) {
+        const int h = q / H, k = q - h * H;
+        wsc[h * 65 + k] = net.W[l][q] * delu_from_a(act[l - 1][k]);
       }
-      int cz = 0;
-      for (int l = 1; l < L; ++l) {
-        const float* w = net.W[l];
-        for (int h = 0; h < H; ++h) {
-          float z = 0.f;
-          for (int k = 0; k < H; ++k) z = fmaf(w[(size_t)h * H + k], delu_from_a(act[l - 1][k]) * ztb[cz][k][d], z);
-          ztb[cz ^ 1][h][d] = z;
-          ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z * z, ud);
-        }
-        cz ^= 1;
+      __syncthreads();  // wsc and Z_{l-1} complete
+      for (int h = hg; h < H; h += 8) {
+        float z = 0.f;
+        for (int k = 0; k < H; ++k) z = fmaf(wsc[h * 65 + k], ztb[cz][k][d], z);
+        ztb[cz ^ 1][h][d] = z;
+        ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z * z, ud);
       }
-      hb[(size_t)i * NXP_MAX + d] = ud;
+      cz ^= 1;
+      __syncthreads();  // before wsc is overwritten
+    }
+    udp[hg][d] = ud;
+    __syncthreads();
+    if (tid < NXP_MAX) {
+      float a = 0.f;
+      for (int g = 0; g < 8; ++g) a += udp[g][tid];
+      hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
     }
     if (tid == 0) fb[i] = Cb;
     return;
