@@ -33,14 +33,15 @@ PEAK_HBM_GBS = 8000.0
 # workloads = BASELINE.json configs; FLOP per path-label from SURVEY.md §8(d)
 WORKLOADS = {
     "burgers": dict(cfg="configs[1]", eq="Cha", widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0,
-                    flop=2.72e5, desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
+                    flop=2.72e5, kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
                                       "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)"),
     "hjb": dict(cfg="configs[2]", eq="OUProcessEquation", widths=[512] * 4, pis=True, points=64, m_per_gpu=4096, K=50,
-                sdgd=0, flop=3.73e6,
+                sdgd=0, flop=3.73e6, kernel="k_pis_rollout + k_gemm_nt chain + k_pis_final + k_reduce per "
+                                            "dpi_label_moments call",
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
                      "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
     "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
-                sdgd=100, flop=3.36e6,
+                sdgd=100, flop=3.36e6, kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
                 desc="Fully-nonlinear case_1 100d (GBM, SDGD v=100), 64 points x 1024 MC paths per GPU, K=50, "
                      "MLP 101-64x3-1 ELU (BASELINE configs[4])"),
 }
@@ -215,7 +216,7 @@ def main():
                        "rel_l2_vs_ref": "<= 3e-7 measured, tolerance 1e-4 (tests/test_gpu_parity.py)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "kernel": "k_paths (+ its 2 small block-reduce kernels) per dpi_label_moments call",
+                         "kernel": wl["kernel"],
                          "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
         }
         if world == 1 and not args.no_cpu_baseline:
