@@ -386,6 +386,75 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
     return y
 
 
+S_HESS_OFFSET = 1e-4  # picard/data.py:848: s = U (T - t) + t + 0.0001 in the Hessian estimator
+
+
+def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512, return_parts=False):
+    """generate_with_gradients_and_hessians (picard/data.py:1220-1223) with K-step EM paths:
+    estimate_terminal_with_gradients_and_hessians_double (:1153-1201) +
+    estimate_integral_with_gradients_and_hessians_double (:823-897).
+
+    The value / gradient columns are the first-order estimators with the reference's two
+    half-steps (their sum is the K-step endpoint) and Y without the extra 1/sqrt(alpha) of the
+    first-order terminal estimator (:1175-1178, :851-864); f is evaluated with the FULL Hessian
+    diagonal (get_f without hessian_approximation_ctx, :1262-1272).  Hessian block (Malliavin
+    weights, antithetic second differences):
+        H = mean_m[ dg_m (N1 N1^T - I) + (T - t) df_m (N2 N2^T - I) ]
+        dg = (g(x + a sqrt(T-t) N1) + g(x - ...) - 2 g(x)) / 2 / (T - t)
+        df = (f(s, x + a sqrt(s-t) N2) + f(s, x - ...) - 2 f(t, x)) / 2 / (s - t)
+    with fresh normals N1 (tag HTERM), N2 (tag HINT).  Returns y (n, 1 + nx + nx^2)."""
+    tx = np.asarray(tx, np.float64)
+    n, nx, T, a = tx.shape[0], eq.nx, eq.T, eq.alpha_sqrt
+    term = np.zeros((n, 1 + nx))
+    integ = np.zeros((n, 1 + nx))
+    hT = np.zeros((n, nx, nx))
+    hI = np.zeros((n, nx, nx))
+    eye = np.eye(nx)
+    for r in range(n):
+        ig = point_base + r
+        t = tx[r, 0]
+        x = tx[r:r + 1, 1:]
+        g_x = eq.g(x)[0, 0]
+        f_b = _f_and_extras(eq, net, np.array([[t]]), x)[0][0, 0]
+        for m0 in range(0, M, m_chunk):
+            m = np.arange(m0, min(M, m0 + m_chunk))
+            B = len(m)
+            S_T, S_s, U, _ = path_noise(eq, ig, m, K, seed, epoch)
+            N1 = px.normals(px.TAG_HTERM, epoch, seed, ig, m, 0, nx)
+            N2 = px.normals(px.TAG_HINT, epoch, seed, ig, m, 0, nx)
+            # terminal, value / gradient (:1166-1183)
+            W_T = math.sqrt((T - t) / K) * S_T
+            c = eq.g(x + a * W_T) - g_x
+            term[r, 0] += c.sum()
+            term[r, 1:] += (c * W_T / (T - t)).sum(0)
+            # terminal Hessian (:1185-1199)
+            W1 = math.sqrt(T - t) * N1
+            dg = (eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g_x) / 2 / (T - t)          # (B, 1)
+            hT[r] += np.einsum("b,bi,bj->ij", dg[:, 0], N1, N1) - dg.sum() * eye
+            # integral, value / gradient (:846-866)
+            s = (U * (T - t) + t + S_HESS_OFFSET)[:, None]
+            W_s = np.sqrt((s - t) / K) * S_s
+            f = _f_and_extras(eq, net, s, x + a * W_s)[0]
+            cI = (T - t) * (f - f_b)
+            integ[r, 0] += cI.sum() + B * f_b * (T - t)
+            integ[r, 1:] += (cI * W_s / (s - t)).sum(0)
+            # integral Hessian (:869-881)
+            W2 = np.sqrt(s - t) * N2
+            fp = _f_and_extras(eq, net, s, x + a * W2)[0]
+            fm = _f_and_extras(eq, net, s, x - a * W2)[0]
+            df = (fp + fm - 2 * f_b) / 2 / (s - t)                                       # (B, 1)
+            hI[r] += (T - t) * (np.einsum("b,bi,bj->ij", df[:, 0], N2, N2) - df.sum() * eye)
+        term[r] /= M
+        integ[r] /= M
+        hT[r] /= M
+        hI[r] /= M
+        term[r, 0] += g_x
+    y = np.concatenate([term + integ, (hT + hI).reshape(n, nx * nx)], -1)
+    if return_parts:
+        return y, np.concatenate([term, hT.reshape(n, -1)], -1), np.concatenate([integ, hI.reshape(n, -1)], -1)
+    return y
+
+
 def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf):
     """picard/data.py:211-223: (tx, clip(y))."""
     tx = sample_points(eq, n, seed, epoch, point_base)

@@ -169,6 +169,27 @@ def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v):
     return items
 
 
+def noise_items_hess(nx, n, M, K, seed, epoch, point_base):
+    """Draw order of sample_with_gradients_and_hessians (picard/data.py:225-237) for a GBM
+    equation: t | x | terminal dW1, dW2 (two half-steps), N1 | s, integral dW1, dW2, N2.  Each
+    pair of half-step normals is injected as S / sqrt(2K) twice, so the two half-steps sum to the
+    K-step endpoint x + a sqrt((tau - t)/K) S."""
+    i = point_base + np.arange(n)
+    items = [("rand", px.uniforms(px.TAG_T, epoch, seed, i, 0)[:, None]),
+             ("randn", px.normals(px.TAG_X, epoch, seed, i, 0, 0, nx))]
+    ii = i[:, None]
+    mm = np.arange(M)[None, :]
+    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, mm, k, nx) for k in range(K)).reshape(n * M, nx)
+    S_s = sum(px.normals(px.TAG_INT, epoch, seed, ii, mm, k, nx) for k in range(K)).reshape(n * M, nx)
+    half = 1.0 / math.sqrt(2 * K)
+    items += [("randn", S_T * half), ("randn", S_T * half),
+              ("randn", px.normals(px.TAG_HTERM, epoch, seed, ii, mm, 0, nx).reshape(n * M, nx)),
+              ("rand", px.uniforms(px.TAG_S, epoch, seed, ii, mm, open_low=True).reshape(n * M, 1)),
+              ("randn", S_s * half), ("randn", S_s * half),
+              ("randn", px.normals(px.TAG_HINT, epoch, seed, ii, mm, 0, nx).reshape(n * M, nx))]
+    return items
+
+
 def make_equation(name, kw, workdir):
     cwd = os.getcwd()
     os.chdir(workdir)
@@ -195,7 +216,7 @@ def state_dict_np(module):
 
 
 def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, point_base=0, v=0,
-             init_seed=0, workdir=None, zero=False, weight_scale=1.0):
+             init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False):
     torch.set_default_dtype(torch.float64)
     eq = make_equation(eq_name, eq_kw, workdir)
     torch.manual_seed(init_seed)
@@ -217,12 +238,17 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
         eq, net, 1, 1, device="cpu", t_always_uniform=True, n_estimate_terminal=M,
         n_estimate_integral=M, hessian_approximation=hess, sample_bound=None,
         estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=0.0)
-    items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v)
-    with NoiseQueue(items):
-        tx, y = gen.sample_with_gradients(n)
+    if hessians:
+        items = noise_items_hess(eq.nx, n, M, K, seed, epoch, point_base)
+        with NoiseQueue(items):
+            tx, y = gen.sample_with_gradients_and_hessians(n)
+    else:
+        items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v)
+        with NoiseQueue(items):
+            tx, y = gen.sample_with_gradients(n)
     out = {
         "case": name, "eq": eq_name, "net": "zero" if zero else net_kind, "n": n, "M": M, "K": K,
-        "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v,
+        "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v, "hessians": hessians,
         "tx": tx.numpy(), "y": y.detach().numpy(),
     }
     for k, val in eq_kw.items():
@@ -242,8 +268,15 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
     print(f"{name}: tx {tx.shape} y {y.shape} |y|={float(y.norm()):.4g}")
 
 
-def main():
+def main(only=None):
     wd = prepare_workdir()
+    global run_case
+    if only:  # regenerate a subset: python make_golden.py <prefix>
+        _rc = run_case
+
+        def run_case(name, *a, **k):  # noqa: F811
+            if name.startswith(only):
+                _rc(name, *a, **k)
     cha = {"nx": 100, "alpha": 1.0, "k": 5.0, "T": 1.0}
     ou = {"nx": 100, "alpha": 1.0, "T": 1.0, "num_components": 5, "mean_scale": 1.0,
           "var_scale": 2.0, "alpha_scale": 4.0}
@@ -264,8 +297,15 @@ def main():
              v=100, workdir=wd)
     run_case("gbm_mlp16_full_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 64, 1, 4,
              workdir=wd)
+    # Malliavin Hessian labels (generate_with_gradients_and_hessians), full-Hessian f
+    run_case("gbm_hess_mlp16_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 64, 2, 6,
+             epoch=1, workdir=wd, hessians=True)
+    run_case("gbm_hess_mlp32x3_K4", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [32] * 3}, 2, 128, 4, 8,
+             epoch=2, point_base=5, workdir=wd, hessians=True)
+    run_case("gbm_hess_zero_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [8]}, 2, 64, 2, 9,
+             workdir=wd, zero=True, hessians=True)
     shutil.rmtree(wd)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -6,12 +6,21 @@ import numpy as np
 from oracle import dpi_oracle as O
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
-CASES = sorted(p.stem for p in GOLDEN.glob("*.npz"))
 
 
 def load(name):
     z = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
     return {k: z[k] for k in z.files}
+
+
+def _is_hess(name):
+    z = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+    return "hessians" in z.files and bool(z["hessians"])
+
+
+_ALL = sorted(p.stem for p in GOLDEN.glob("*.npz"))
+CASES = [c for c in _ALL if not _is_hess(c)]       # sample_with_gradients fixtures
+HESS_CASES = [c for c in _ALL if _is_hess(c)]      # sample_with_gradients_and_hessians fixtures
 
 
 def oracle_equation(f):
