@@ -602,6 +602,7 @@ struct LdsGbm {
   float fst[4 * P * NSG];
   float wx[NSG];
   float tau[P], cmul[P], bsh[P], fbp[P];
+  float smt[P];                    // Hessian labels: s - t per path
   unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
 };
 
@@ -981,11 +982,190 @@ struct PathArgs {
   uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
   int order;  // phase order policy (k_paths)
   int split;  // fused MLP on the fp16-split MFMA
+  float* hpart;            // Hessian labels: block sums [n][nbp][nx*nx]
+  uint32_t c3h1, c3h2;     // Hessian labels: Malliavin normal streams (tags HTERM, HINT)
 };
 
+// ------------------------------------------------------------------------------ Hessian labels
+// Malliavin-weight Hessian block of generate_with_gradients_and_hessians (picard/data.py:1220-1223;
+// terminal :1185-1199, integral :869-881), per 64-path block, after phase 3 of k_paths:
+//   H_blk = sum_p [ aI_p (N2 N2^T - I) + aT_p (N1 N1^T - I) ]
+//   aI = (T-t) (f(s, x + a sqrt(s-t) N2) + f(s, x - ...) - 2 f_b) / 2 / (s-t)     (full Hessian f)
+//   aT = (g(x + a sqrt(T-t) N1) + g(x - ...) - 2 g(x)) / 2 / (T-t)
+// N1, N2: fresh normals (tags HTERM / HINT, k = 0), written into the noise tile in turn; the
+// outer-product sums are (nx x 64) (64 x nx) products on v_mfma_f32_16x16x4_f32 over the upper
+// triangle of 16 x 16 tiles (wave w owns tiles w, w+4, ...), mirrored on store.
+template <int H, int L>
+__device__ __forceinline__ void hess_accum(LdsGbm<H>& sh, const float* wgt, int NT, floatx4 (&acc)[9]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, jj = lane & 15, qq = lane >> 4;
+  const int ntiles = NT * (NT + 1) / 2;
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) {
+    const int q = wv + 4 * sl;
+    if (q < ntiles) {
+      int I = 0, r = q;
+      while (r >= NT - I) {
+        r -= NT - I;
+        ++I;
+      }
+      const int J = I + r;
+      const float* ra = sh.S + (16 * I + jj) * SS + qq;
+      const float* rb = sh.S + (16 * J + jj) * SS + qq;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[sl] = mfma4(ra[4 * t] * wgt[4 * t + qq], rb[4 * t], acc[sl]);
+    }
+  }
+}
+
+template <int KIND, int H, int L, bool ZERO>
+__device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, const PathArgs& a, LdsGbm<H>& sh,
+                                           int i, int blk, uint32_t ig, uint32_t m, float s, float smt, float tmt,
+                                           float g_x, int nxp) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
+  const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2, NT = nxp / 16;
+  // f at (s, x + cmul S) with the full Hessian diagonal (get_f without SDGD, data.py:1262-1272);
+  // valid in the lanes of group qq == 0 for path pp
+  auto f_eval = [&]() -> float {
+    float s1 = 0.f, s2 = 0.f;
+    if (!ZERO) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+    const float c1 = 0.5f * (1.0f - e.alpha), c2 = 0.25f;
+    float arg[NSG], sn[NSG];
+    const float spp = sh.tau[pp], cpp = sh.cmul[pp];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      arg[c] = 0.f;
+      if (c < e.nodes) {
+        const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
+                          sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
+        arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+      }
+      sn[c] = __sinf(arg[c]);
+    }
+    const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
+    return c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+  };
+  float* wgt = sh.bsh;  // per-path weights of the current outer-product term
+  floatx4 acc[9];
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) acc[sl] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- integral term: N2 -> noise tile, w . N2 for the exact-solution terms
+  __syncthreads();  // phase 3 is done with the integral noise tile
+  {
+    float fs[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) fs[c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = wv + 4 * c;
+      if (j < nb) {
+        const f4 z = normals4(philox4x32_10((uint32_t)j, m, ig, a.c3h2, a.k0, a.k1));
+        const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          const float v = d < nx ? zz[q] : 0.f;
+          sh.S[d * SS + lane] = v;
+          if (d < nx)
+#pragma unroll
+            for (int c2 = 0; c2 < NSG; ++c2)
+              if (c2 < e.nodes) fs[c2] = fmaf(e.gw[c2 * F + 1 + d], v, fs[c2]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fs[c];
+  }
+  const float cw = e.asq * sqrtf(smt);
+  if (wv == 0) {
+    sh.cmul[lane] = cw;
+    sh.smt[lane] = smt;
+  }
+  __syncthreads();
+  const float fplus = f_eval();
+  __syncthreads();
+  if (wv == 0) sh.cmul[lane] = -cw;
+  __syncthreads();
+  const float fminus = f_eval();
+  const float fbp = sh.fbp[pp];
+  if (qq == 0) wgt[pp] = tmt * ((fplus + fminus - 2.f * fbp) * 0.5f / sh.smt[pp]);  // path pp, not this lane's
+  __syncthreads();
+  const float aI = wgt[lane];  // lane = path
+  hess_accum<H, L>(sh, wgt, NT, acc);
+
+  // ---- terminal term: N1 -> noise tile, g(x +- a sqrt(T-t) N1)
+  __syncthreads();  // every wave is done reading N2 and the weights
+  float gp[NSG], gm[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) gp[c] = gm[c] = 0.f;
+  const float cw1 = e.asq * sqrtf(tmt);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int j = wv + 4 * c;
+    if (j < nb) {
+      const f4 z = normals4(philox4x32_10((uint32_t)j, m, ig, a.c3h1, a.k0, a.k1));
+      const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        const float v = d < nx ? zz[q] : 0.f;
+        sh.S[d * SS + lane] = v;
+        if (d < nx) {
+          Eq<KIND>::gstat(e, d, fmaf(cw1, v, sh.xsh[d]), gp);
+          Eq<KIND>::gstat(e, d, fmaf(-cw1, v, sh.xsh[d]), gm);
+        }
+      }
+    }
+  }
+  auto wave_stats = [&](float (&st)[NSG]) -> float {  // g from the 4 waves' partial statistics
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = st[c];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      st[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
+               sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
+    __syncthreads();
+    return Eq<KIND>::gfin(e, st);
+  };
+  const float gplus = wave_stats(gp);
+  const float gminus = wave_stats(gm);
+  const float aT = (gplus + gminus - 2.f * g_x) * 0.5f / tmt;
+  if (wv == 0) wgt[lane] = aT;
+  __syncthreads();
+  hess_accum<H, L>(sh, wgt, NT, acc);
+
+  // ---- identity part, store (upper tiles mirrored)
+  const float dsum = wave_sum(aI + aT);
+  float* out = a.hpart + ((size_t)i * a.nbp + blk) * (size_t)nx * nx;
+  const int ntiles = NT * (NT + 1) / 2;
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) {
+    const int q = wv + 4 * sl;
+    if (q < ntiles) {
+      int I = 0, r = q;
+      while (r >= NT - I) {
+        r -= NT - I;
+        ++I;
+      }
+      const int J = I + r;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int d1 = 16 * I + 4 * qq + rr, d2 = 16 * J + jj;
+        if (d1 < nx && d2 < nx && d1 <= d2) {  // upper triangle, mirrored: exactly symmetric labels
+          const float v = acc[sl][rr] - (d1 == d2 ? dsum : 0.f);
+          out[(size_t)d1 * nx + d2] = v;
+          if (d1 != d2) out[(size_t)d2 * nx + d1] = v;
+        }
+      }
+    }
+  }
+}
+
 // One workgroup = (point i, 64 consecutive MC indices).  See the file header.
-template <int KIND, int H, int L, bool ZERO, bool SPLIT>
-__global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false>
+__global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+  static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
@@ -1047,12 +1227,15 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
   }
   // s ~ U(t, T] for this lane's path (data.py:359); integral/terminal step multipliers
   const float U = u01_oc(philox4x32_10(0u, m, ig, a.c3s, a.k0, a.k1).x);
-  const float s = fmaf(U, tmt, t);
-  const float smt = U * tmt;  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
+  // Hessian labels: s = U (T - t) + t + 1e-4 (data.py:848) and Y without the first-order
+  // terminal estimator's extra 1/sqrt(alpha) (data.py:1175-1178, :851-864)
+  const float smt = U * tmt + (HESS ? 1e-4f : 0.f);  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
+  const float s = HESS ? t + smt : fmaf(U, tmt, t);
+  const float ya = HESS ? 1.f : e.asq;
   const float cI = e.asq * sqrtf(smt / Kf);            // X_s = x + cI * sum_k xi_k
-  const float yI = 1.0f / (sqrtf(Kf * smt) * e.asq);    // Y_s = yI * sum_k xi_k   (data.py:520)
+  const float yI = 1.0f / (sqrtf(Kf * smt) * ya);      // Y_s = yI * sum_k xi_k   (data.py:520)
   const float cT = e.asq * sqrtf(tmt / Kf);
-  const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq);    // Y_T (data.py:917)
+  const float yT = 1.0f / (sqrtf(Kf * tmt) * ya);      // Y_T (data.py:917)
   if (wv == 0) {
     sh.tau[lane] = s;
     sh.cmul[lane] = cI;
@@ -1297,6 +1480,7 @@ __global__ __launch_bounds__(256, 2) void k_paths(EqDev e, NetDev net, PathArgs 
       }
     }
   }
+  if constexpr (HESS) hess_block<KIND, H, L, ZERO>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
 }
 
 // Canonical fixed-order sum of `cnt` values (stride `stride`): zero-pad to a power of two
@@ -1333,7 +1517,8 @@ __device__ __forceinline__ float tree_sum(const float* __restrict__ p, int cnt, 
 // partial [n][2F][nbp] -> moments [n][2F] (and, if y != nullptr, the finalized labels).
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
                                                 float* __restrict__ moments, const float* __restrict__ gx,
-                                                float invM, int add_g, float bound, float* __restrict__ y) {
+                                                float invM, int add_g, float bound, float* __restrict__ y,
+                                                int ystride) {
   const int i = blockIdx.x;
   const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
   if (c >= 2 * F) return;
@@ -1343,9 +1528,21 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
     if (y && c < F) {
       float v = s * invM;
       if (c == 0 && add_g) v += gx[i];
-      y[(size_t)i * F + c] = fminf(fmaxf(v, -bound), bound);
+      y[(size_t)i * ystride + c] = fminf(fmaxf(v, -bound), bound);
     }
   }
+}
+
+// Hessian block sums [n][nbp][C] -> y[:, off:off+C] = clip(sum / M): one wave per (point, column),
+// the canonical tree over blocks.
+__global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int C, int nbp,
+                                                     float invM, float bound, float* __restrict__ y, int ystride,
+                                                     int yoff) {
+  const int i = blockIdx.y;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const float s = tree_sum(hpart + (size_t)i * nbp * C + c, nbp, (size_t)C);
+  if ((threadIdx.x & 63) == 0) y[(size_t)i * ystride + yoff + c] = fminf(fmaxf(s * invM, -bound), bound);
 }
 
 // parts [G][len] -> out [len]
@@ -2009,6 +2206,7 @@ struct Launch {
   const PathArgs* a;
   int nblocks;
   hipStream_t st;
+  bool hess = false;  // k_paths in Hessian-label mode (GBM only)
 };
 
 template <int KIND, int H, int L, bool Z>
@@ -2016,7 +2214,14 @@ static void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch
   if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                        q.bx, q.hb);
-  else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+  else if (q.hess) {
+    if constexpr (KIND == DPI_EQ_GBM) {
+      EqDev e2 = p->e;
+      e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
+                         *q.a);
+    }
+  } else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
     if (q.a->split)
       hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
     else
@@ -2203,7 +2408,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   }
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
-                     (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y);
+                     (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -2253,6 +2458,75 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
   // moments and labels come out of the same block-reduce launch
   return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, moments, ws, ws_bytes, stream, y,
                       sample_bound);
+}
+
+// ---- Malliavin Hessian labels (generate_with_gradients_and_hessians)
+static size_t hess_extra(int n, int M, int nx, size_t* moff) {
+  const size_t nbp = (size_t)(M + P - 1) / P;
+  *moff = al256((size_t)n * nbp * nx * nx * 4);  // Hessian block sums, then the moments
+  return *moff + al256((size_t)n * 2 * (1 + nx) * 4);
+}
+
+size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M) {
+  if (!p || n < 0 || M < 0) return 0;
+  size_t moff;
+  return al256(ws_layout(net, n, M, 1 + p->e.nx).total) + hess_extra(n, M, p->e.nx, &moff);
+}
+
+int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
+                                             uint64_t seed, uint32_t epoch, uint32_t point_base, float sample_bound,
+                                             float* y, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (p->e.kind != DPI_EQ_GBM)
+    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
+  if (net->d.kind == 2) return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: MLP or ZeroSolution networks only");
+  if (!tx || !y || !ws || n < 0 || K < 1 || M < P || (M % P) || M > 1024 * P || epoch > 0xFFFFFFu)
+    return fail(DPI_ERR_ARG, "generate_with_gradients_and_hessians: bad arguments (M multiple of 64, <= 65536)");
+  if (n == 0) return 0;
+  const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = M / P;
+  const WsLayout w = ws_layout(net, n, M, F);
+  size_t moff;
+  const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);
+  if (ws_bytes < need) return fail(DPI_ERR_WORKSPACE, "workspace too small (dpi_workspace_bytes_hessians)");
+  if ((rc = dpi_point_baseline(p, net, tx, n, ws, ws_bytes, stream))) return rc;
+  char* b = (char*)ws;
+  PathArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.tx = tx;
+  a.gx = (const float*)(b + w.gx);
+  a.fb = (const float*)(b + w.fb);
+  a.bx = (const float*)(b + w.bx);
+  a.hb = (const float*)(b + w.hb);
+  a.partial = (float*)(b + w.partial);
+  a.n = n;
+  a.nbp = nbp;
+  a.m_begin = 0;
+  a.K = K;
+  a.flags = DPI_BOTH;
+  a.k0 = (uint32_t)seed;
+  a.k1 = (uint32_t)(seed >> 32);
+  a.c3t = DPI_TAG_TERM | (epoch << 8);
+  a.c3s = DPI_TAG_S | (epoch << 8);
+  a.c3i = DPI_TAG_INT | (epoch << 8);
+  a.c3q = DPI_TAG_SDGD | (epoch << 8);
+  a.c3h1 = DPI_TAG_HTERM | (epoch << 8);
+  a.c3h2 = DPI_TAG_HINT | (epoch << 8);
+  a.point_base = point_base;
+  a.hpart = (float*)(b + base);
+  hipStream_t st = (hipStream_t)stream;
+  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
+  q.hess = true;
+  if (!dispatch_any(p, net, q))
+    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
+  HIPCHK(hipGetLastError());
+  float* moments = (float*)(b + base + moff);
+  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
+                     1.0f / (float)M, 1, sample_bound, y, F + C);
+  hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, 1.0f / (float)M,
+                     sample_bound, y, F + C, F);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 }  // extern "C"

@@ -133,6 +133,16 @@ class OnlineDataGenerator:
         tx, pb = self.sample_t_and_x(n_batch)
         return tx, self._generate(tx, pb, _lib.DPI_BOTH)
 
+    def sample_with_gradients_and_hessians(self, n_batch):
+        """data.py:225-237: (tx, clip(u_ux_uxx)) with u_ux_uxx (n, 1 + nx + nx^2)."""
+        tx, pb = self.sample_t_and_x(n_batch)
+        return tx, self._generate_hess(tx, pb, self.sample_bound)
+
+    def generate_with_gradients_and_hessians(self, tx, point_base=None):
+        """data.py:1220-1223: Malliavin-weight Hessian labels (no clip), (n, 1 + nx + nx^2)."""
+        pb = self._take_points(tx.shape[0]) if point_base is None else point_base
+        return self._generate_hess(self._as_points(tx), pb, float("inf"))
+
     def generate_with_gradients(self, tx, point_base=None):
         """data.py:1208-1218: terminal + integral estimators at given points (no clip)."""
         pb = self._take_points(tx.shape[0]) if point_base is None else point_base
@@ -189,6 +199,20 @@ class OnlineDataGenerator:
         return out
 
     # ------------------------------------------------------------------ internals
+    def _generate_hess(self, tx, pb, bound):
+        if self.n_estimate_terminal != self.n_estimate_integral:
+            raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
+        n, nx, M = tx.shape[0], self.equation.nx, self.n_estimate_integral
+        need = self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.dpi_generate_with_gradients_and_hessians(
+            self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, bound, _ptr(y),
+            _ptr(self._ws), self._ws.numel(), _stream(self.device)), "dpi_generate_with_gradients_and_hessians")
+        return y
+
+
     def _as_points(self, tx):
         if tx.device != self.device or tx.dtype != torch.float32 or not tx.is_contiguous():
             tx = tx.to(device=self.device, dtype=torch.float32).contiguous()

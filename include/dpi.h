@@ -154,6 +154,23 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
                                 float sample_bound, float* y, float* moments, void* ws, size_t ws_bytes,
                                 void* stream);
 
+/* Malliavin-weight Hessian labels: replaces
+ *   _OnlineDataGenerator.sample_with_gradients_and_hessians (picard/data.py:225-237, after its
+ *   draws 1-2) -> OnlineDataGenerator.generate_with_gradients_and_hessians (:1220-1223) =
+ *   estimate_terminal_with_gradients_and_hessians_double (:1153-1201) +
+ *   estimate_integral_with_gradients_and_hessians_double (:823-897), with the clip of :236.
+ * y: (n, 1 + nx + nx*nx) = [u, grad u, Hessian (row-major)], f evaluated with the full Hessian
+ * diagonal whatever the problem's SDGD setting (the reference calls get_f without the SDGD
+ * context there).  GBMEquationComplexExact problems (the reference asserts
+ * SimpleDiffusionEquationWithHessian), MLP (width <= 64) or zero networks; M % 64 == 0, M <= 65536.
+ * Noise: the first-order streams plus N1 = tag DPI_TAG_HTERM, N2 = tag DPI_TAG_HINT (k = 0).
+ * ws >= dpi_workspace_bytes_hessians(p, net, n, M). */
+size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
+int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
+                                             uint64_t seed, uint32_t epoch, uint32_t point_base,
+                                             float sample_bound, float* y, void* ws, size_t ws_bytes,
+                                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -246,3 +246,58 @@ def test_unsupported_configurations_fail_loudly():
         dpi.OnlineDataGenerator(dpi.GBMEquationComplexExact(100), dpi.construct_mlp(101, 1, [128] * 2, ["ELU"] * 2, None),
                                 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
                                 n_estimate_integral=64).sample_with_gradients(2)
+
+
+# ----------------------------------------------------------------------------- Hessian labels
+from golden_util import HESS_CASES  # noqa: E402
+
+
+def _blocks(y, nx):
+    return {"value": (slice(None), slice(0, 1)), "grad": (slice(None), slice(1, 1 + nx)),
+            "hess": (slice(None), slice(1 + nx, None))}
+
+
+@pytest.mark.parametrize("case", HESS_CASES)
+def test_hessian_labels_golden_reference_parity(case):
+    """generate_with_gradients_and_hessians (picard/data.py:1220-1223) on the GPU vs the
+    reference's own output on the same noise (tests/golden/make_golden.py), per block."""
+    f = load(case)
+    eq = product_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    y = gen.generate_with_gradients_and_hessians(tx, point_base=int(f["point_base"])).cpu().numpy()
+    nx = eq.nx
+    assert y.shape == f["y"].shape
+    for name, sl in _blocks(y, nx).items():
+        r = O.rel_l2(y[sl], f["y"][sl])
+        assert r < TOL, (name, r)
+
+
+def test_hessian_labels_config5_network_vs_oracle():
+    """Config-5 network (3 x 64 ELU), K = 10, M = 256, against the fp64 oracle; the Hessian block
+    is symmetric by construction."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    net = _random_mlp(eq, [64] * 3, 12)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                  n_estimate_integral=256, n_euler_steps=10, seed=13, epoch=4,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": 100}})
+    tx, y = gen.sample_with_gradients_and_hessians(2)
+    oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+    ref = O.labels_grad_hess(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 256, 10, 13, 4, 0)
+    y = y.cpu().numpy()
+    for name, sl in _blocks(y, 100).items():
+        r = O.rel_l2(y[sl], ref[sl])
+        assert r < TOL, (name, r)
+    h = y[:, 101:].reshape(2, 100, 100)
+    assert np.array_equal(h, np.transpose(h, (0, 2, 1)))
+
+
+def test_hessian_labels_need_gbm():
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd._lib import DPIError
+    eq = dpi.Cha(10, 1.0, 5.0, 1.0)
+    gen = dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(1), 1, 1, device="cuda:0", t_always_uniform=True,
+                                  n_estimate_terminal=64, n_estimate_integral=64, n_euler_steps=2)
+    with pytest.raises(DPIError):
+        gen.sample_with_gradients_and_hessians(2)
