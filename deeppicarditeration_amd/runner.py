@@ -9,7 +9,9 @@ Per Picard iteration i:
      tensors (SURVEY.md §8f rank 2);
   2. fit: N_EPOCHS of shuffled mini-batches, value loss weighted by exp(beta t)
      (picard/solution.py:75-82), plus the gradient loss of PicardSolutionGradientWrapper with a
-     FixedLossScaler (picard/solution_jac.py:71-82, 167-213) when its weight > 0 — PyTorch-ROCm;
+     FixedLossScaler (picard/solution_jac.py:71-82, 167-213) when its weight > 0, or — with
+     TRAIN.SUPERVISE_HESSIAN — gradient + Hessian losses of PicardSolutionGradientHessianWrapper with
+     a FixedHessianLossScaler (solution_jac.py:85-109, 219-259) on Malliavin Hessian labels;
   3. checkpoint model_{i}.pt; the trained network becomes the next iteration's u.
 Iteration 1 uses ZeroSolution (picard_iteration.py:182).
 """
@@ -27,19 +29,21 @@ from .solution import PISGradNet, ZeroSolution, construct_mlp
 
 
 class LabelBuffer:
-    """Device-resident (tx, y) label store for one Picard iteration."""
+    """Device-resident (tx, y) label store for one Picard iteration; y is (u, u_x) or, with
+    hessians=True, (u, u_x, u_xx) of generate_with_gradients_and_hessians (data.py:225-237)."""
 
-    def __init__(self, gen, n_total, points_per_call):
+    def __init__(self, gen, n_total, points_per_call, hessians=False):
         self.gen = gen
         self.n_total = int(n_total)
         self.ppc = max(1, min(int(points_per_call), self.n_total))
+        self.sample = gen.sample_with_gradients_and_hessians if hessians else gen.sample_with_gradients
 
     def fill(self):
         txs, ys = [], []
         done = 0
         while done < self.n_total:
             n = min(self.ppc, self.n_total - done)
-            tx, y = self.gen.sample_with_gradients(n)
+            tx, y = self.sample(n)
             txs.append(tx)
             ys.append(y)
             done += n
@@ -61,10 +65,9 @@ class PicardRunner:
             raise NotImplementedError(f"METHOD.cls={cfg.METHOD.cls}: only the DPI (Picard) method is built")
         if cfg.PICARD.FORMULA == "TwoLayer":
             raise NotImplementedError("PICARD.FORMULA=TwoLayer is out of scope")
-        if cfg.TRAIN.SUPERVISE_HESSIAN:
-            raise NotImplementedError("TRAIN.SUPERVISE_HESSIAN labels are not built yet")
         self.equation = getattr(eqs, cfg.EQUATION.cls)(**cfg.EQUATION.kwargs)  # picard_iteration.py:90-92
         self.supervise_gradient = bool(cfg.TRAIN.SUPERVISE_GRADIENT or self.equation.has_gradient_term)
+        self.supervise_hessian = bool(cfg.TRAIN.SUPERVISE_HESSIAN)  # picard_iteration.py:160, :114
         if cfg.NETWORK.TYPE != "Value":
             raise NotImplementedError("NETWORK.TYPE must be 'Value' for the device label path")
         self.N = cfg.PICARD.N
@@ -93,7 +96,7 @@ class PicardRunner:
             hessian_approximation=d.HESSIAN_APPROXIMATION, sample_bound=d.SAMPLE_BOUND,
             estimate_terminal=d.ESTIMATE_TERMINAL, estimate_integral=d.ESTIMATE_INTEGRAL,
             estimate_delta_t=d.ESTIMATE_DELTA_T, n_euler_steps=d.EULER_STEPS, seed=d.SEED)
-        return LabelBuffer(gen, d.DATA_SIZE, d.POINTS_PER_CALL).fill()
+        return LabelBuffer(gen, d.DATA_SIZE, d.POINTS_PER_CALL, hessians=self.supervise_hessian).fill()
 
     # ------------------------------------------------------------------ fit
     def fit(self, net, tx, y):
@@ -104,11 +107,21 @@ class PicardRunner:
         if t.LOSS.FN.cls is not None:  # LossFnLinearClip (solution.py:22-33)
             clip = float(t.LOSS.FN.kwargs["clip"])
             loss_fn = lambda x: torch.where(x.abs() < clip, x * x, 2 * clip * x.abs() - clip ** 2)  # noqa: E731
-        gw = 0.0
-        if self.supervise_gradient and t.LOSS.SCALER.cls == "FixedLossScaler":
-            gw = float(t.LOSS.SCALER.kwargs.get("fixed_weight", 0.0))
+        gw, hw = 0.0, 0.0
+        kw = t.LOSS.SCALER.kwargs
+        if self.supervise_hessian:  # FixedHessianLossScaler (solution_jac.py:85-109)
+            if t.LOSS.SCALER.cls != "FixedHessianLossScaler":
+                raise NotImplementedError("SUPERVISE_HESSIAN needs LOSS.SCALER.cls = FixedHessianLossScaler")
+            gw, hw = float(kw["fixed_gradient_weight"]), float(kw["fixed_hessian_weight"])
+        elif self.supervise_gradient and t.LOSS.SCALER.cls == "FixedLossScaler":
+            gw = float(kw.get("fixed_weight", 0.0))
         elif self.supervise_gradient and t.LOSS.SCALER.cls is not None:
             raise NotImplementedError(f"loss scaler {t.LOSS.SCALER.cls}")
+        nx = self.equation.nx
+        n_hess_samples = int(t.NUM_HESS_SAMPLES)
+        hess_fn = None
+        if self.supervise_hessian:  # vmap(hessian(forward)) (solution_jac.py:128)
+            hess_fn = torch.func.vmap(torch.func.hessian(lambda z: net(z[None])[0, 0]))
         n = tx.shape[0]
         bs = int(t.BATCH_SIZE) if t.BATCH_SIZE else n
         last = float("nan")
@@ -118,12 +131,25 @@ class PicardRunner:
                 idx = perm[b0:b0 + bs]
                 xb, yb = tx[idx].detach(), y[idx]
                 w = torch.exp(xb[:, :1] * beta)
-                if gw > 1e-9:  # PicardSolutionGradientWrapper (solution_jac.py:167-213)
+                if self.supervise_hessian:  # PicardSolutionGradientHessianWrapper (solution_jac.py:219-259)
+                    xb.requires_grad_(True)
+                    u = net(xb)
+                    ux = torch.autograd.grad(u.sum(), xb, create_graph=True)[0][:, 1:]
+                    uh = hess_fn(xb)[:, 1:, 1:].reshape(xb.shape[0], nx * nx)
+                    diff = uh - yb[:, 1 + nx:]
+                    if n_hess_samples > 0:
+                        idx_h = torch.randperm(nx * nx, device=xb.device)[:n_hess_samples]
+                        diff = diff[:, idx_h]
+                    v_loss = torch.mean(w * loss_fn(u - yb[:, :1]))
+                    g_loss = torch.mean(w * loss_fn(ux - yb[:, 1:1 + nx]), dim=0).sum()
+                    h_loss = torch.mean(w * loss_fn(diff), dim=0).sum()
+                    loss = v_loss + gw * g_loss + hw * h_loss
+                elif gw > 1e-9:  # PicardSolutionGradientWrapper (solution_jac.py:167-213)
                     xb.requires_grad_(True)
                     u = net(xb)
                     ux = torch.autograd.grad(u.sum(), xb, create_graph=True)[0][:, 1:]
                     v_loss = torch.mean(w * loss_fn(u - yb[:, :1]))
-                    g_loss = torch.mean(w * loss_fn(ux - yb[:, 1:]), dim=0).sum()
+                    g_loss = torch.mean(w * loss_fn(ux - yb[:, 1:1 + nx]), dim=0).sum()
                     loss = v_loss + gw * g_loss
                 else:  # PicardBaseSolution.training_step (solution.py:75-82)
                     loss = torch.mean(w * loss_fn(net(xb) - yb[:, :1]))

@@ -63,3 +63,47 @@ def test_label_buffer_is_device_resident(tmp_path):
     tx, y = runner.labels()
     assert tx.is_cuda and y.is_cuda and tx.shape == (1024, 9) and y.shape == (1024, 9)
     assert torch.isfinite(y).all()
+
+
+GBM_HESS = """NAME: {name}
+EQUATION:
+  cls: GBMEquationComplexExact
+  kwargs: {{nx: 100, alpha: 1.0, T: 1.0}}
+PICARD: {{N: 2}}
+FORCE: true
+DATA:
+  DATA_SIZE: 256
+  POINTS_PER_CALL: 128
+  EULER_STEPS: 4
+  kwargs: {{t_always_uniform: true, n_estimate_terminal: 128, n_estimate_integral: 128}}
+TRAIN:
+  N_EPOCHS: 2
+  BATCH_SIZE: 64
+  SUPERVISE_GRADIENT: true
+  SUPERVISE_HESSIAN: true
+  NUM_HESS_SAMPLES: 500
+  LOSS: {{beta: 0.0, SCALER: {{cls: FixedHessianLossScaler, kwargs: {{fixed_gradient_weight: 0.1, fixed_hessian_weight: 0.01}}}}}}
+NETWORK:
+  NEURONS: [32, 32]
+  ACTIVATIONS: [ELU, ELU]
+  BOUND: None
+  RELOAD: true
+EVAL: {{L2_N_POINTS: 256}}
+"""
+
+
+def test_picard_train_gbm_hessian_supervision(tmp_path):
+    """TRAIN.SUPERVISE_HESSIAN: Malliavin Hessian labels (n, 1 + nx + nx^2) from the device path
+    feed the gradient + Hessian loss of PicardSolutionGradientHessianWrapper."""
+    f = tmp_path / "gbm.yaml"
+    f.write_text(GBM_HESS.format(name=tmp_path / "run"))
+    runner = PicardRunner(load_cfg(str(f)))
+    runner.i = 1
+    tx, y = runner.labels()
+    assert y.shape == (256, 1 + 100 + 100 * 100) and torch.isfinite(y).all()
+    h = y[:, 101:].reshape(-1, 100, 100)
+    assert torch.equal(h, h.transpose(1, 2))
+    runner.i = 0
+    hist = runner.run()
+    assert [h_["iter"] for h_ in hist] == [1, 2]
+    assert all(h_["loss"] == h_["loss"] for h_ in hist) and all(h_["rel_l2_u"] is not None for h_ in hist)
