@@ -40,6 +40,12 @@ WORKLOADS = {
                                             "dpi_label_moments call",
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
                      "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
+    "gbm_hess": dict(cfg="configs[4] stretch (Malliavin Hessian labels)", eq="GBMEquationComplexExact", widths=[64] * 3,
+                     points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6,
+                     kernel="k_paths<GBM,64,3,hessians> + k_reduce + k_reduce_hess per dpi_label_moments_hessians call",
+                     desc="Fully-nonlinear case_1 100d (GBM), generate_with_gradients_and_hessians: labels "
+                          "(u, u_x, u_xx) = 1 + 100 + 10,000 wide, full-Hessian f at 3 points per path, 64 points x "
+                          "1024 MC paths per GPU, K=50, MLP 101-64x3-1 ELU"),
     "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
                 sdgd=100, flop=3.36e6, kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
                 desc="Fully-nonlinear case_1 100d (GBM, SDGD v=100), 64 points x 1024 MC paths per GPU, K=50, "
@@ -99,8 +105,11 @@ def cpu_baseline(wl, sample_paths, target_s=10.0):
     with threadpool_limits(limits=1):  # the restatement is a scalar port: one thread, BLAS included
         while True:
             tx = O.sample_points(oeq, 1, seed=1, point_base=pts)
-            O.labels_grad(oeq, onet, tx, sample_paths, wl["K"], 1, 0, pts, v=wl["sdgd"],
-                          m_chunk=min(sample_paths, 256))
+            if wl.get("hess"):
+                O.labels_grad_hess(oeq, onet, tx, sample_paths, wl["K"], 1, 0, pts, m_chunk=min(sample_paths, 256))
+            else:
+                O.labels_grad(oeq, onet, tx, sample_paths, wl["K"], 1, 0, pts, v=wl["sdgd"],
+                              m_chunk=min(sample_paths, 256))
             done += sample_paths
             pts += 1
             dt = time.perf_counter() - t0
@@ -147,7 +156,11 @@ def main():
     def step():
         tx, pb = gen.sample_t_and_x(N_POINTS)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        y = labeler.labels(tx, pb, on_moments_begin=lambda: e0.record(), on_moments_end=lambda: e1.record())
+        if wl.get("hess"):
+            y = labeler.labels_hessians(tx, pb, on_moments_begin=lambda: e0.record(),
+                                        on_moments_end=lambda: e1.record())
+        else:
+            y = labeler.labels(tx, pb, on_moments_begin=lambda: e0.record(), on_moments_end=lambda: e1.record())
         ev.append((e0, e1))
         return y
 

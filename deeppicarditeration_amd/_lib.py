@@ -50,6 +50,11 @@ SIGNATURES = {
                                             c_uint32, c_int, c_float, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),
     "dpi_workspace_bytes_hessians": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
+    "dpi_label_moments_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
+                                           c_uint32, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dpi_label_finalize_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
+                                            c_size_t, c_void_p]),
+    "dpi_sums_reduce": (c_int, [c_void_p, c_int, c_size_t, c_void_p, c_void_p]),
     "dpi_generate_with_gradients_and_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64,
                                                          c_uint32, c_uint32, c_float, c_void_p, c_void_p, c_size_t,
                                                          c_void_p]),

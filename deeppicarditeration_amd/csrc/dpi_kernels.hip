@@ -1536,13 +1536,25 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
 // Hessian block sums [n][nbp][C] -> y[:, off:off+C] = clip(sum / M): one wave per (point, column),
 // the canonical tree over blocks.
 __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int C, int nbp,
-                                                     float invM, float bound, float* __restrict__ y, int ystride,
-                                                     int yoff) {
+                                                     float* __restrict__ hsum, float invM, float bound,
+                                                     float* __restrict__ y, int ystride, int yoff) {
   const int i = blockIdx.y;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   const float s = tree_sum(hpart + (size_t)i * nbp * C + c, nbp, (size_t)C);
-  if ((threadIdx.x & 63) == 0) y[(size_t)i * ystride + yoff + c] = fminf(fmaxf(s * invM, -bound), bound);
+  if ((threadIdx.x & 63) == 0) {
+    if (hsum) hsum[(size_t)i * C + c] = s;
+    if (y) y[(size_t)i * ystride + yoff + c] = fminf(fmaxf(s * invM, -bound), bound);
+  }
+}
+
+// Hessian sums (n, C) -> y[:, off:off+C] = clip(sum / M)
+__global__ void k_finalize_hess(const float* __restrict__ hsum, int n, int C, float invM, float bound,
+                                float* __restrict__ y, int ystride, int yoff) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)n * C) return;
+  const size_t i = gid / C, c = gid - i * C;
+  y[i * ystride + yoff + c] = fminf(fmaxf(hsum[gid] * invM, -bound), bound);
 }
 
 // parts [G][len] -> out [len]
@@ -1552,6 +1564,16 @@ __global__ __launch_bounds__(256) void k_reduce_parts(const float* __restrict__ 
   if (c >= len) return;
   const float s = tree_sum(parts + c, G, (size_t)len);
   if ((threadIdx.x & 63) == 0) out[c] = s;
+}
+
+__global__ void k_finalize_y(const float* moments, const float* gx, int n, int F, float invM, int add_g,
+                             float bound, float* y, int ystride) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * F) return;
+  const int i = gid / F, c = gid - i * F;
+  float v = moments[(size_t)i * 2 * F + c] * invM;
+  if (c == 0 && add_g) v += gx[i];
+  y[(size_t)i * ystride + c] = fminf(fmaxf(v, -bound), bound);
 }
 
 __global__ void k_finalize(const float* moments, const float* gx, int n, int F, float invM, int add_g, float bound,
@@ -2431,6 +2453,16 @@ int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, voi
   return 0;
 }
 
+int dpi_sums_reduce(const float* parts, int n_parts, size_t len, float* out, void* stream) {
+  if (!parts || !out || n_parts < 1 || n_parts > 1024 || len > 0x7fffffffu)
+    return fail(DPI_ERR_ARG, "sums_reduce: bad arguments (1 <= n_parts <= 1024)");
+  if (len == 0) return 0;
+  hipLaunchKernelGGL(k_reduce_parts, dim3((unsigned)((len + 3) / 4)), dim3(256), 0, (hipStream_t)stream, parts,
+                     n_parts, (int)len, out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int dpi_label_finalize(dpi_problem p, const float* moments, int n, int M, int flags, float sample_bound, float* y,
                        const void* ws, size_t ws_bytes, void* stream) {
   if (!p || !moments || !y || !ws || n < 0 || M < 1 || ws_bytes < (size_t)n * 4)
@@ -2473,23 +2505,24 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M) {
   return al256(ws_layout(net, n, M, 1 + p->e.nx).total) + hess_extra(n, M, p->e.nx, &moff);
 }
 
-int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
-                                             uint64_t seed, uint32_t epoch, uint32_t point_base, float sample_bound,
-                                             float* y, void* ws, size_t ws_bytes, void* stream) {
+static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                             uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments, float* hsum,
+                             void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
   int rc = check_pair(p, net);
   if (rc) return rc;
   if (p->e.kind != DPI_EQ_GBM)
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
   if (net->d.kind == 2) return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: MLP or ZeroSolution networks only");
-  if (!tx || !y || !ws || n < 0 || K < 1 || M < P || (M % P) || M > 1024 * P || epoch > 0xFFFFFFu)
-    return fail(DPI_ERR_ARG, "generate_with_gradients_and_hessians: bad arguments (M multiple of 64, <= 65536)");
+  if (!tx || !ws || !moments || n < 0 || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
+      (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu)
+    return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
   if (n == 0) return 0;
-  const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = M / P;
+  const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
+  if (nbp > 1024) return fail(DPI_ERR_ARG, "Hessian labels: at most 1024 x 64 paths per call");
   const WsLayout w = ws_layout(net, n, M, F);
   size_t moff;
   const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);
   if (ws_bytes < need) return fail(DPI_ERR_WORKSPACE, "workspace too small (dpi_workspace_bytes_hessians)");
-  if ((rc = dpi_point_baseline(p, net, tx, n, ws, ws_bytes, stream))) return rc;
   char* b = (char*)ws;
   PathArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -2501,7 +2534,7 @@ int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const f
   a.partial = (float*)(b + w.partial);
   a.n = n;
   a.nbp = nbp;
-  a.m_begin = 0;
+  a.m_begin = m_begin;
   a.K = K;
   a.flags = DPI_BOTH;
   a.k0 = (uint32_t)seed;
@@ -2520,13 +2553,57 @@ int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const f
   if (!dispatch_any(p, net, q))
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());
-  float* moments = (float*)(b + base + moff);
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
-                     1.0f / (float)M, 1, sample_bound, y, F + C);
-  hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, 1.0f / (float)M,
-                     sample_bound, y, F + C, F);
+                     1.0f / (float)M, 1, bound, y, F + C);
+  hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
+                     1.0f / (float)M, bound, y, F + C, F);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments,
+                               float* hessian_sums, void* ws, size_t ws_bytes, void* stream) {
+  if (!hessian_sums) return fail(DPI_ERR_ARG, "label_moments_hessians: null hessian_sums");
+  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, moments, hessian_sums, ws,
+                           ws_bytes, stream, nullptr, 0.f);
+}
+
+int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M,
+                                float sample_bound, float* y, void* ws, size_t ws_bytes, void* stream) {
+  if (!p || !moments || !hessian_sums || !y || !ws || n < 0 || M < 1)
+    return fail(DPI_ERR_ARG, "label_finalize_hessians: bad arguments");
+  if (n == 0) return 0;
+  const int nx = p->e.nx, F = 1 + nx, C = nx * nx;
+  if (ws_bytes < (size_t)n * 4) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const float* gx = (const float*)ws;  // WsLayout: gx at offset 0 (written by dpi_point_baseline)
+  hipLaunchKernelGGL(k_finalize_y, dim3((n * F + 255) / 256), dim3(256), 0, st, moments, gx, n, F, 1.0f / (float)M,
+                     1, sample_bound, y, F + C);
+  const size_t tot = (size_t)n * C;
+  hipLaunchKernelGGL(k_finalize_hess, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, hessian_sums, n, C,
+                     1.0f / (float)M, sample_bound, y, F + C, F);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
+                                             uint64_t seed, uint32_t epoch, uint32_t point_base, float sample_bound,
+                                             float* y, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (!y || M < P || (M % P) || M > 1024 * P)
+    return fail(DPI_ERR_ARG, "generate_with_gradients_and_hessians: bad arguments (M multiple of 64, <= 65536)");
+  if (n == 0) return 0;
+  if (p->e.kind != DPI_EQ_GBM)
+    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
+  if ((rc = dpi_point_baseline(p, net, tx, n, ws, ws_bytes, stream))) return rc;
+  const WsLayout w = ws_layout(net, n, M, 1 + p->e.nx);
+  size_t moff;
+  hess_extra(n, M, p->e.nx, &moff);
+  float* moments = (float*)((char*)ws + al256(w.total) + moff);
+  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, moments, nullptr, ws, ws_bytes, stream,
+                           y, sample_bound);
 }
 
 }  // extern "C"

@@ -108,8 +108,10 @@ class OnlineDataGenerator:
         self._ws = None
 
     # ------------------------------------------------------------------ buffers
-    def _workspace(self, n, M):
+    def _workspace(self, n, M, hessians=False):
         need = self.lib.dpi_workspace_bytes(self.problem, self.net.handle, n, M)
+        if hessians:
+            need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
@@ -164,10 +166,10 @@ class OnlineDataGenerator:
         return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
-    def point_baseline(self, tx):
+    def point_baseline(self, tx, hessians=False):
         n = tx.shape[0]
         M = max(self.n_estimate_terminal, self.n_estimate_integral)
-        ws = self._workspace(n, M)
+        ws = self._workspace(n, M, hessians)
         _lib.check(self.lib.dpi_point_baseline(self.problem, self.net.handle, _ptr(tx), n, _ptr(ws), ws.numel(),
                                                _stream(self.device)), "dpi_point_baseline")
         return ws
@@ -188,6 +190,33 @@ class OnlineDataGenerator:
         _lib.check(self.lib.dpi_label_finalize(self.problem, _ptr(moments), n, M, flags, b, _ptr(y), _ptr(ws),
                                                ws.numel(), _stream(self.device)), "dpi_label_finalize")
         return y
+
+    def label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
+        """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2)."""
+        n, nx = tx.shape[0], self.equation.nx
+        mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self.device)
+        hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self.device)
+        _lib.check(self.lib.dpi_label_moments_hessians(
+            self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, point_base, m_begin, m_end,
+            _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_label_moments_hessians")
+        return mom, hs
+
+    def finalize_hessians(self, moments, hsums, M, ws, bound=None):
+        n, nx = moments.shape[0], self.equation.nx
+        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self.device)
+        b = self.sample_bound if bound is None else bound
+        _lib.check(self.lib.dpi_label_finalize_hessians(self.problem, _ptr(moments), _ptr(hsums), n, M, b, _ptr(y),
+                                                        _ptr(ws), ws.numel(), _stream(self.device)),
+                   "dpi_label_finalize_hessians")
+        return y
+
+    def sums_reduce(self, parts):
+        """(G, ...) per-rank sums -> (...), the canonical fixed-order tree over ranks."""
+        parts = parts.contiguous()
+        out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
+        _lib.check(self.lib.dpi_sums_reduce(_ptr(parts), parts.shape[0], out.numel(), _ptr(out), _stream(self.device)),
+                   "dpi_sums_reduce")
+        return out
 
     def moments_reduce(self, parts):
         """(G, n, 2, 1+nx) per-rank moments -> (n, 2, 1+nx), fixed pairwise order (parts is scratch)."""

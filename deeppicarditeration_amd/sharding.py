@@ -36,6 +36,31 @@ class ShardedLabeler:
         dist.all_gather_into_tensor(flat, mom, group=self.group)  # rank-major concatenation
         return self.gen.moments_reduce(flat.view((self.world,) + tuple(mom.shape)))
 
+    def gather_sums(self, x):
+        """All-gather per-rank sums (any shape) and reduce them in canonical rank order."""
+        if self.world == 1:
+            return x
+        import torch.distributed as dist
+        x = x.contiguous()
+        flat = torch.empty((self.world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(flat, x, group=self.group)
+        return self.gen.sums_reduce(flat.view((self.world,) + tuple(x.shape)))
+
+    def labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
+        """generate_with_gradients_and_hessians for tx with this rank's MC shard (n, 1 + nx + nx^2);
+        identical on every rank.  Exchange: the (n, 2, 1+nx) moments and (n, nx^2) Hessian sums."""
+        M = self.gen.n_estimate_integral
+        if self.gen.n_estimate_terminal != M:
+            raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
+        ws = self.gen.point_baseline(tx, hessians=True)
+        m0, m1 = self.shard(M)
+        if on_moments_begin:
+            on_moments_begin()
+        mom, hs = self.gen.label_moments_hessians(tx, point_base, M, m0, m1, ws)
+        if on_moments_end:
+            on_moments_end()
+        return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
+
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""
         from . import _lib

@@ -22,6 +22,10 @@
  *   dpi_label_finalize       picard/data.py:924-926, :525-526, :222  mean over M, + g(x), clip
  *   dpi_generate_with_gradients  picard/data.py:1208-1218 (baseline + moments + finalize)
  *   dpi_moments_reduce       (no reference counterpart: fixed-order combine of per-rank moments)
+ *   dpi_generate_with_gradients_and_hessians  picard/data.py:1220-1223 (+ :1153-1201, :823-897, :225-237)
+ *   dpi_label_moments_hessians / dpi_label_finalize_hessians  the same, split for MC sharding
+ *   dpi_sums_reduce          (no reference counterpart: fixed-order combine of per-rank sums)
+ *   dpi_set_gemm_precision   (no reference counterpart: MFMA precision of the network evaluation)
  */
 #ifndef DPI_H_
 #define DPI_H_
@@ -166,6 +170,21 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
  * Noise: the first-order streams plus N1 = tag DPI_TAG_HTERM, N2 = tag DPI_TAG_HINT (k = 0).
  * ws >= dpi_workspace_bytes_hessians(p, net, n, M). */
 size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
+
+/* Sharding building blocks of the Hessian labels (the first-order dpi_label_moments pattern):
+ * after dpi_point_baseline, the sums over m in [m_begin, m_end) of the value/gradient
+ * contributions and their squares (moments (n, 2, 1+nx)) and of the Hessian contributions
+ * (hessian_sums (n, nx*nx)); dpi_label_finalize_hessians turns (possibly rank-reduced) sums into
+ * y (n, 1 + nx + nx*nx) = clip(sums / M [+ g(x)]). */
+int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments,
+                               float* hessian_sums, void* ws, size_t ws_bytes, void* stream);
+int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M,
+                                float sample_bound, float* y, void* ws, size_t ws_bytes, void* stream);
+
+/* out[j] = canonical tree sum over the n_parts rows of parts (n_parts, len) (the rank-reduce of
+ * dpi_moments_reduce for any flat length; parts is read-only). */
+int dpi_sums_reduce(const float* parts, int n_parts, size_t len, float* out, void* stream);
 int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K,
                                              uint64_t seed, uint32_t epoch, uint32_t point_base,
                                              float sample_bound, float* y, void* ws, size_t ws_bytes,

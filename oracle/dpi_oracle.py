@@ -494,6 +494,35 @@ def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0):
     return c, g_x
 
 
+def path_contributions_hess(eq, net, tx_row, ig, m, K, seed, epoch=0):
+    """Per-path rows of the Hessian-label estimator (labels_grad_hess): value/gradient c
+    (len(m), 1+nx), Hessian h (len(m), nx*nx) whose means (+ g(x) in c[:, 0]) are the label."""
+    t = float(tx_row[0])
+    x = np.asarray(tx_row[1:], np.float64)[None]
+    T, a, nx = eq.T, eq.alpha_sqrt, eq.nx
+    m = np.asarray(m)
+    g_x = eq.g(x)[0, 0]
+    f_b = _f_and_extras(eq, net, np.array([[t]]), x)[0][0, 0]
+    S_T, S_s, U, _ = path_noise(eq, ig, m, K, seed, epoch)
+    N1 = px.normals(px.TAG_HTERM, epoch, seed, ig, m, 0, nx)
+    N2 = px.normals(px.TAG_HINT, epoch, seed, ig, m, 0, nx)
+    W_T = math.sqrt((T - t) / K) * S_T
+    cT = eq.g(x + a * W_T) - g_x
+    s = (U * (T - t) + t + S_HESS_OFFSET)[:, None]
+    W_s = np.sqrt((s - t) / K) * S_s
+    cI = (T - t) * (_f_and_extras(eq, net, s, x + a * W_s)[0] - f_b)
+    c = np.concatenate([cT + cI + f_b * (T - t), cT * W_T / (T - t) + cI * W_s / (s - t)], -1)
+    W1 = math.sqrt(T - t) * N1
+    aT = ((eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g_x) / 2 / (T - t))[:, 0]
+    W2 = np.sqrt(s - t) * N2
+    fp = _f_and_extras(eq, net, s, x + a * W2)[0]
+    fm = _f_and_extras(eq, net, s, x - a * W2)[0]
+    aI = (T - t) * ((fp + fm - 2 * f_b) / 2 / (s - t))[:, 0]
+    h = (aT[:, None, None] * (N1[:, :, None] * N1[:, None, :] - np.eye(nx))
+         + aI[:, None, None] * (N2[:, :, None] * N2[:, None, :] - np.eye(nx)))
+    return c, h.reshape(len(m), nx * nx), g_x
+
+
 def tree_sum_f32(values):
     """The device's canonical fixed-order sum (csrc/dpi_kernels.hip tree_sum): zero-pad to a
     power of two >= 64 and add as a perfect binary tree in index order, in fp32.  values: (cnt, ...)."""

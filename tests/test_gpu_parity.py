@@ -301,3 +301,27 @@ def test_hessian_labels_need_gbm():
                                   n_estimate_terminal=64, n_estimate_integral=64, n_euler_steps=2)
     with pytest.raises(DPIError):
         gen.sample_with_gradients_and_hessians(2)
+
+
+def test_hessian_labels_shard_invariance_and_determinism():
+    """Config-5 network, 8 points x 1024 paths: Hessian labels are bitwise reproducible, the
+    MC-sharded sums (G = 2, 4, 8) + dpi_sums_reduce equal the single call bit for bit, and
+    moments + finalize equal the one-call generate_with_gradients_and_hessians."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    net = _random_mlp(eq, [64] * 3, 14)
+    M = 1024
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=8, seed=3, epoch=2)
+    tx, _ = gen.sample_t_and_x(8, point_base=0)
+    ws = gen.point_baseline(tx, hessians=True)
+    mom, hs = gen.label_moments_hessians(tx, 0, M, 0, M, ws)
+    mom2, hs2 = gen.label_moments_hessians(tx, 0, M, 0, M, ws)
+    assert torch.equal(mom, mom2) and torch.equal(hs, hs2)
+    for G in (2, 4, 8):
+        parts = [gen.label_moments_hessians(tx, 0, M, r * M // G, (r + 1) * M // G, ws) for r in range(G)]
+        assert torch.equal(gen.sums_reduce(torch.stack([p[0] for p in parts])), mom), G
+        assert torch.equal(gen.sums_reduce(torch.stack([p[1] for p in parts])), hs), G
+    y = gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"))
+    y1 = gen.generate_with_gradients_and_hessians(tx, point_base=0)
+    assert torch.equal(y, y1)

@@ -97,3 +97,82 @@ def test_two_rank_gloo_labels_equal_single_rank():
     # and the labels are the oracle's labels (to fp32 summation error)
     ref = O.labels_grad(eq, net, tx, M, K, 7)
     assert O.rel_l2(single, ref) < 1e-5
+
+
+# ----------------------------------------------------------------------------- Hessian labels
+MH, KH, NH = 256, 2, 2
+
+
+def _problem_hess():
+    from pathlib import Path
+    d = Path(__file__).resolve().parents[1] / "deeppicarditeration_amd" / "problem_data"
+    eq = O.GBMEquationComplexExact(NX, np.load(d / "gbm_2nodes_w_100d_case_1.npy"),
+                                   np.load(d / "gbm_2nodes_v_100d_case_1.npy"))
+    rng = np.random.default_rng(1)
+    net = O.MLP([rng.normal(0, 0.1, (16, NX + 1)), rng.normal(0, 0.25, (1, 16))],
+                [rng.normal(0, 0.1, 16), rng.normal(0, 0.1, 1)], ["ELU"])
+    return eq, net, O.sample_points(eq, NH, seed=9)
+
+
+class OracleGenHess:
+    """Stands in for the Hessian-label building blocks of OnlineDataGenerator."""
+
+    def __init__(self, eq, net):
+        self.eq, self.net = eq, net
+        self.n_estimate_terminal = self.n_estimate_integral = MH
+        self.gx = None
+
+    def point_baseline(self, tx, hessians=False):
+        assert hessians
+        return tx
+
+    def label_moments_hessians(self, tx, point_base, M_, m0, m1, ws):
+        n = tx.shape[0]
+        mom = np.zeros((n, 2, NX + 1), np.float32)
+        hs = np.zeros((n, NX * NX), np.float32)
+        gx = []
+        for r in range(n):
+            c, h, g = O.path_contributions_hess(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), KH, 9)
+            gx.append(g)
+            cb, hb = c.reshape(-1, 64, NX + 1), h.reshape(-1, 64, NX * NX)
+            mom[r, 0] = O.tree_sum_f32(np.stack([O.tree_sum_f32(b.astype(np.float32)) for b in cb]))
+            mom[r, 1] = O.tree_sum_f32(np.stack([O.tree_sum_f32(b.astype(np.float32) ** 2) for b in cb]))
+            hs[r] = O.tree_sum_f32(np.stack([O.tree_sum_f32(b.astype(np.float32)) for b in hb]))
+        self.gx = np.array(gx)
+        return torch.from_numpy(mom), torch.from_numpy(hs)
+
+    def sums_reduce(self, parts):
+        return torch.from_numpy(O.tree_sum_f32(parts.numpy()))
+
+    def finalize_hessians(self, mom, hs, M_, ws):
+        y = mom[:, 0].numpy() / M_
+        y[:, 0] += self.gx
+        return torch.from_numpy(np.concatenate([y, hs.numpy() / M_], -1))
+
+
+def _worker_hess(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem_hess()
+    y = ShardedLabeler(OracleGenHess(eq, net), rank=rank, world=world).labels_hessians(tx, 0)
+    q.put((rank, y.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_hessian_labels_equal_single_rank():
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem_hess()
+    single = ShardedLabeler(OracleGenHess(eq, net), 0, 1).labels_hessians(tx, 0).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30000 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_hess, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0].tobytes() == res[1].tobytes() == single.tobytes()
+    ref = O.labels_grad_hess(eq, net, tx, MH, KH, 9)
+    assert O.rel_l2(single, ref) < 1e-5

@@ -11,7 +11,7 @@ from pathlib import Path
 
 src, tag = Path(sys.argv[1]), sys.argv[2]
 dst = Path(__file__).resolve().parents[1] / "profiles"
-for wl in ("burgers", "hjb", "gbm"):
+for wl in ("burgers", "hjb", "gbm", "gbm_hess"):
     f = src / f"trace_{wl}" / "trace_kernel_stats.csv"
     if f.exists():
         rows = list(csv.DictReader(open(f)))

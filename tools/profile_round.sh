@@ -10,7 +10,8 @@ export TMPDIR=/tmp
 tools/gpu_check.sh 300 $out/bench_burgers.log python bench.py --steps 50 --warmup 5
 tools/gpu_check.sh 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
 tools/gpu_check.sh 300 $out/bench_gbm.log python bench.py --workload gbm --steps 20 --warmup 3
-for wl in burgers gbm hjb; do
+tools/gpu_check.sh 300 $out/bench_gbm_hess.log python bench.py --workload gbm_hess --steps 10 --warmup 2
+for wl in burgers gbm gbm_hess hjb; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_$wl -o trace --output-format csv -- \
     python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_$wl.log 2>&1
 done
