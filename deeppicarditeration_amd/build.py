@@ -1,18 +1,25 @@
-"""Build libdpi_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+"""Build libdpi_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+Four translation units (the C-ABI / PIS / reduce TU and one k_paths family per equation) compile
+in parallel to objects, then link into one shared library."""
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 REPO = ROOT.parent
-SRC = ROOT / "csrc" / "dpi_kernels.hip"
+CSRC = ROOT / "csrc"
+UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_gbm.hip"]
+OBJ = ROOT / "build"
 OUT = ROOT / "libdpi_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", f"-I{REPO / 'include'}"]
 
 
 def sources():
-    return [SRC] + sorted((ROOT / "csrc").glob("*.h")) + [REPO / "include" / "dpi.h"]
+    return [CSRC / u for u in UNITS] + sorted(CSRC.glob("*.h")) + [REPO / "include" / "dpi.h"]
 
 
 def needs_build():
@@ -25,8 +32,19 @@ def needs_build():
 def build(force=False, verbose=True):
     if not force and not needs_build():
         return OUT
-    cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{REPO / 'include'}",
-           "-o", str(OUT), str(SRC)]
+    OBJ.mkdir(exist_ok=True)
+
+    def compile_unit(u):
+        obj = OBJ / (Path(u).stem + ".o")
+        cmd = [HIPCC, *FLAGS, "-c", "-o", str(obj), str(CSRC / u)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(UNITS)) as ex:
+        objs = list(ex.map(compile_unit, UNITS))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

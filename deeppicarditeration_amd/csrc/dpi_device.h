@@ -1,0 +1,1488 @@
+// MI355X (gfx950) device code of the DPI label-generation hot path (kernels as templates; the
+// C-ABI host code is dpi_kernels.hip, the k_paths instantiations dpi_paths_*.hip).
+#pragma once
+//
+// One workgroup (256 threads = 4 waves) owns one collocation point i and 64 consecutive
+// Monte-Carlo indices m.  Per workgroup:
+//   phase 1  (VALU)  Philox4x32-10 + Box–Muller noise, K-step Euler–Maruyama rollout of the
+//                    terminal path (t -> T) and the integral path (t -> s), 100 dims each.
+//                    Lane = path; a wave owns whole 4-dim blocks, so Philox counters other
+//                    than m are wave-uniform.  Terminal sums stay in registers, integral
+//                    sums go to LDS as the MFMA B operand; g(X_T) statistics are reduced
+//                    over waves in fixed order.
+//   phase 2  (MFMA)  u(s, X_s) and its input gradient for the 64 paths: the MLP as
+//                    v_mfma_f32_16x16x4_f32 tiles, hidden x paths orientation (wave = 16
+//                    paths), activations kept in registers as the next layer's B operand,
+//                    weights staged through LDS 32 rows at a time, backward via the
+//                    transposed weights.  X_s = x + c_p S is never formed: layer 1 is
+//                    z = (W1x x + b1) + W1t s + c_p (W1x S).
+//   phase 3          per-path contributions (g(X_T)-g(x))(1,Y_T) + (T-t)(f-f_b)(1,Y_s)
+//                    reduced over the 64 lanes into a per-(point, block) partial slab.
+// A pairwise reduce kernel then sums the blocks in a fixed tree (bit-reproducible; equal
+// for any split of the blocks over GPUs aligned to powers of two) and a finalize kernel
+// divides by M, adds g(x) and clips (picard/data.py:924-926, :525-526, :222).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <type_traits>
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/dpi.h"
+#include "dpi_eq.h"
+#include "dpi_rng.h"
+
+namespace dpi {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int P = DPI_PATH_BLOCK;  // 64 paths per workgroup
+constexpr int NTH = 256;           // threads per workgroup
+constexpr int SS = P + 4;          // LDS row stride of the [dim][path] noise tile (bank-conflict free)
+constexpr int WST = 136;           // LDS row stride of a staged weight chunk (WST/4 = 2 mod 4)
+constexpr int NXP_MAX = 128;       // max padded state dimension
+constexpr int HMAX = 128;
+
+struct NetDev {
+  int kind;  // 0 zero, 1 mlp
+  int H, L, nxp;
+  const float* W1x;   // (H, nxp)   W1[:, 1:]
+  const float* w1t;   // (H)        W1[:, 0]
+  const float* b1;    // (H)
+  const float* c1;    // (H)        sum_d W1[h, 1+d]
+  const float* W1xT;  // (nxp, H)
+  const float* W[4];  // (H, H) hidden layer l = 1..L-1
+  const float* WT[4];
+  const float* b[4];
+  const float* wout;  // (H)
+  float bout;
+  // fp16-split copies (x = hi + 2^-11 lo) in MFMA fragment order, see pack_split():
+  int nxp32;                 // nx padded to 32
+  const uint32_t* W1xS;      // (H, nxp32)
+  const uint32_t* W1xTS;     // (nxp32, H)
+  const uint32_t* WS[4];     // (H, H)
+  const uint32_t* WTS[4];
+};
+
+// ------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float elu(float z) { return z > 0.f ? z : __expf(z) - 1.0f; }
+__device__ __forceinline__ float delu_from_a(float a) { return a > 0.f ? 1.0f : a + 1.0f; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// gfx950 cross-half / cross-row lane swaps (VALU, no LDS): for the pair (a, b) the two results
+// sum to [a_lo + a_hi | b_lo + b_hi] (halves of 32 lanes) resp. the same over rows of 16 lanes.
+__device__ __forceinline__ float swap32_sum(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_sum(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// sum over the 4 lane groups (lanes j, j+16, j+32, j+48) of the MFMA C layout
+__device__ __forceinline__ float qsum(float v) {
+  v = swap32_sum(v, v);
+  return swap16_sum(v, v);
+}
+// Column sums of a 64 x 64 block: v[c] is lane l's value of column c; on return lane l holds the
+// sum over all 64 lanes of column l.  A halving butterfly: at level m = 32, 16, ..., 1 a lane
+// keeps the lower half of its columns if (lane & m) == 0, else the upper half, and adds its
+// partner's copy of the kept half — 63 exchanges for 64 columns instead of 6 per column.  The
+// summation order of every column is fixed (independent of which block or rank runs it).
+template <int M>
+__device__ __forceinline__ float dpp_take(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), M, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float column_sums64(float (&v)[64]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = swap32_sum(v[j], v[j + 32]);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = swap16_sum(v[j], v[j + 16]);
+  // within rows of 16: partners by row_mirror (i <-> 15 - i), row_half_mirror (i <-> 7 - i),
+  // quad_perm [2,3,0,1] and [1,0,3,2]; the side is the lane bit m in every case
+#define DPI_BFLY(MASK, H, CTRL)                                  \
+  _Pragma("unroll") for (int j = 0; j < H; ++j) {                \
+    const bool up = (lane & MASK) != 0;                          \
+    const float keep = up ? v[j + H] : v[j];                     \
+    const float send = up ? v[j] : v[j + H];                     \
+    v[j] = keep + dpp_take<CTRL>(send);                          \
+  }
+  DPI_BFLY(8, 8, 0x140)
+  DPI_BFLY(4, 4, 0x141)
+  DPI_BFLY(2, 2, 0x4E)
+  DPI_BFLY(1, 1, 0xB1)
+#undef DPI_BFLY
+  return v[0];
+}
+
+// Stage rows [r0, r0 + nrows) of a row-major global matrix with ncol floats per row
+// (ncol % 4 == 0) into LDS rows of stride WST.
+__device__ __forceinline__ void stage_rows(const float* __restrict__ g, int ncol, int r0, int nrows, float* wsh) {
+  const int nf4 = ncol >> 2;
+  for (int idx = threadIdx.x; idx < nrows * nf4; idx += NTH) {
+    const int r = idx / nf4, c = idx - r * nf4;
+    const float4 v = *reinterpret_cast<const float4*>(g + (size_t)(r0 + r) * ncol + 4 * c);
+    *reinterpret_cast<float4*>(wsh + r * WST + 4 * c) = v;
+  }
+}
+
+// ---------------- fp16-split MFMA (v_mfma_f32_16x16x32_f16, three products per fp32 product)
+// x = hi + 2^-11 lo with hi = fp16(x), lo = fp16((x - hi) 2^11): a (x) b = hi_a hi_b + 2^-11 (hi_a lo_b
+// + lo_a hi_b) + O(2^-22 |a b|).  Split matrices are packed per row as chunks of 32 columns; chunk
+// u holds, for each lane group q = 0..3, 8 hi then 8 lo halves of columns
+// k(q, j) = 32u + 4q + (j & 3) + 16 (j >> 2), j = 0..7 — exactly the columns whose activations a
+// lane of group q holds in the 16x16 C layout of tiles 2u and 2u+1, so activations become the B
+// operand without any data movement.
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
+constexpr float SPLIT_LO = 2048.0f, SPLIT_INV = 1.0f / 2048.0f;
+
+__device__ __forceinline__ floatx4 mfma16(half8 a, half8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split8(const float (&x)[8], half8& hi, half8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)x[j];
+    hi[j] = h;
+    lo[j] = (_Float16)((x[j] - (float)h) * SPLIT_LO);
+  }
+}
+// B operand of chunk u from activation tiles 2u, 2u+1 held in the C layout.
+__device__ __forceinline__ void split_act(const float (&t0)[4], const float (&t1)[4], half8& hi, half8& lo) {
+  const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  split8(x, hi, lo);
+}
+// Split chunks sit in LDS unpadded (C words per row, as LDS-DMA writes 1 KiB lane-linear per wave
+// instruction) with the 16-B granules of row r XOR-swizzled: granule g is stored at g ^ (r & m),
+// m = min(15, C/4 - 1).  The 16 lanes of each ds_read_b128 lane group then hit distinct banks.
+__device__ __forceinline__ int split_swz(int C) { return C >= 64 ? 15 : (C >> 2) - 1; }
+__device__ __forceinline__ void load_a_split(const uint32_t* wsh, int C, int row, int u, int q, half8& ah,
+                                             half8& al) {
+  const int m = split_swz(C), g = 8 * u + 2 * q, x = row & m;
+  const uint32_t* rp = wsh + row * C;
+  ah = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp + 4 * (g ^ x)));
+  al = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp + 4 * ((g + 1) ^ x)));
+}
+// 32 output rows (tiles T0, T0+1) of W B for a staged 32-row chunk; B pre-split per chunk u.
+template <int NU>
+__device__ __forceinline__ void split_rows32(const uint32_t* wsh, int C, int jj, int qq, const half8 (&bh)[NU],
+                                             const half8 (&bl)[NU], floatx4 (&out)[2]) {
+  floatx4 am[2], ac[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      half8 ah, al;
+      load_a_split(wsh, C, 16 * t + jj, u, qq, ah, al);
+      am[t] = mfma16(ah, bh[u], am[t]);
+      ac[t] = mfma16(ah, bl[u], ac[t]);
+      ac[t] = mfma16(al, bh[u], ac[t]);
+    }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[t][r] = fmaf(ac[t][r], SPLIT_INV, am[t][r]);
+}
+
+}  // namespace dpi
+#include "dpi_gemm.h"
+#include "dpi_pis.h"
+namespace dpi {
+
+// LDS layout (floats) shared by the baseline and path kernels.
+struct Lds {
+  float S[NXP_MAX * SS];   // [dim][path] integral noise sums (path kernel) / x tile (baseline)
+  float W[2 * 32 * HMAX];  // weight chunk: f32 rows of stride WST, or two split chunks (LDS-DMA ring)
+  float vec[4 * HMAX];     // base0 | w1t | wout | c1
+  float bh[4 * HMAX];      // hidden-layer biases
+  float xsh[NXP_MAX];      // point x (path kernel) / zeros (baseline)
+  float gst[4 * P * NSG];  // per-wave partial g statistics
+  float tau[P], cmul[P], bsh[P];
+};
+
+// ------------------------------------------------------------------------------ MLP tile
+// u and gradient terms for the 16 paths of this wave (path column pp = 16*wave + (lane&15)).
+// Inputs (all in LDS): S tile [d][p], xsh (X_d = xsh[d] + cmul_p * S[d][p]), tau (time input),
+// cmul, vec[0:H] = base0 (layer-1 bias incl. W1x x), vec[H:2H] = w1t, vec[2H:3H] = wout,
+// vec[3H:4H] = c1, bh[l*H:(l+1)*H] = biases of hidden layers l >= 1.
+// If bx_out != nullptr (baseline mode) writes b1 + W1x S (per path) to bx_out[pp*bstride + h].
+template <int KIND, int H, int L, class SH>
+__device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& sh, int nxt, float& u_out,
+                                         float& gsum_out, float& gA_out, float& gB_out, float* bx_out,
+                                         int bstride, int n_valid_paths) {
+  constexpr int HT = H / 16;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  float act[L][HT][4];
+
+  // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+#pragma unroll
+  for (int T0 = 0; T0 < HT; T0 += 2) {
+    const int nr = (HT - T0) >= 2 ? 32 : 16;
+    __syncthreads();
+    stage_rows(net.W1x, net.nxp, 16 * T0, nr, sh.W);
+    __syncthreads();
+#pragma unroll
+    for (int T2 = 0; T2 < 2; ++T2) {
+      const int T = T0 + T2;
+      if (T < HT) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+        for (int t = 0; t < nxt; ++t) {
+          const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+          const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+          acc = mfma4(a.x, bc[0], acc);
+          acc = mfma4(a.y, bc[SS], acc);
+          acc = mfma4(a.z, bc[2 * SS], acc);
+          acc = mfma4(a.w, bc[3 * SS], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int h = 16 * T + 4 * qq + r;
+          const float z = fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h]));
+          act[0][T][r] = elu(z);
+          if (bx_out && pp < n_valid_paths) bx_out[(size_t)pp * bstride + h] = sh.vec[h] + acc[r];
+        }
+      }
+    }
+  }
+  // ---------------- hidden layers
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      const int nr = (HT - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.W[l], H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < HT) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[l - 1][t][0], acc);
+            acc = mfma4(a.y, act[l - 1][t][1], acc);
+            acc = mfma4(a.z, act[l - 1][t][2], acc);
+            acc = mfma4(a.w, act[l - 1][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = 16 * T + 4 * qq + r;
+            act[l][T][r] = elu(acc[r] + sh.bh[l * H + h]);
+          }
+        }
+      }
+    }
+  }
+  // ---------------- output u = wout . a_L + bout ; delta_L = wout * elu'(a_L)
+  float up = 0.f;
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      const float w = sh.vec[2 * H + h];
+      up = fmaf(w, act[L - 1][T][r], up);
+      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+    }
+  u_out = qsum(up) + net.bout;
+  // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      const int nr = (HT - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.WT[l + 1], H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < HT) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[l + 1][t][0], acc);
+            acc = mfma4(a.y, act[l + 1][t][1], acc);
+            acc = mfma4(a.z, act[l + 1][t][2], acc);
+            acc = mfma4(a.w, act[l + 1][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) act[l][T][r] = acc[r] * delu_from_a(act[l][T][r]);
+        }
+      }
+    }
+  }
+  // ---------------- input gradient
+  if (!Eq<KIND>::GRAD_FULL) {
+    float gp = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp = fmaf(sh.vec[3 * H + 16 * T + 4 * qq + r], act[0][T][r], gp);
+    gsum_out = qsum(gp);
+    gA_out = gB_out = 0.f;
+  } else {
+    float A = 0.f, B = 0.f;
+    for (int T0 = 0; T0 < nxt; T0 += 2) {
+      const int nr = (nxt - T0) >= 2 ? 32 : 16;
+      __syncthreads();
+      stage_rows(net.W1xT, H, 16 * T0, nr, sh.W);
+      __syncthreads();
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < nxt) {
+          floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+#pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+            acc = mfma4(a.x, act[0][t][0], acc);
+            acc = mfma4(a.y, act[0][t][1], acc);
+            acc = mfma4(a.z, act[0][t][2], acc);
+            acc = mfma4(a.w, act[0][t][3], acc);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = 16 * T + 4 * qq + r;
+            if (d < e.nx) {
+              const float X = fmaf(cm, sh.S[d * SS + pp], sh.xsh[d]);
+              Eq<KIND>::gacc(e, d, X, acc[r], A, B);
+            }
+          }
+        }
+      }
+    }
+    gA_out = qsum(A);
+    gB_out = qsum(B);
+    gsum_out = 0.f;
+  }
+}
+
+// Weight-chunk stream of the split MLP: every 32-row chunk of every matrix, in use order, is
+// copied global -> LDS by LDS-DMA one chunk ahead into a two-slot ring (the copy overlaps the
+// MFMAs of the current chunk; no registers, one barrier per chunk).
+// Chunk index -> (matrix, C, row offset): layer 1 (W1x), hidden layers (W_l), backward
+// (W_{l+1}^T, l = L-2..0), then — GRAD_FULL only — the input gradient (W1x^T).
+template <int H, int L>
+struct SplitStream {
+  static constexpr int NT = H / 32;  // chunks per H-row matrix
+  const NetDev& net;
+  int C1, n1, nT1, total;
+  __device__ SplitStream(const NetDev& n, bool grad_full) : net(n) {
+    C1 = n.nxp32;
+    n1 = NT;                               // layer-1 chunks (H output rows)
+    nT1 = C1 / 32;                         // W1x^T chunks (C1 output rows)
+    total = n1 + 2 * (L - 1) * NT + (grad_full ? nT1 : 0);
+  }
+  __device__ __forceinline__ void desc(int idx, const uint32_t*& g, int& C, int& r0) const {
+    if (idx < n1) {
+      g = net.W1xS, C = C1, r0 = 32 * idx;
+      return;
+    }
+    idx -= n1;
+    if (idx < (L - 1) * NT) {
+      g = net.WS[1 + idx / NT], C = H, r0 = 32 * (idx % NT);
+      return;
+    }
+    idx -= (L - 1) * NT;
+    if (idx < (L - 1) * NT) {
+      g = net.WTS[L - 1 - idx / NT], C = H, r0 = 32 * (idx % NT);
+      return;
+    }
+    idx -= (L - 1) * NT;
+    g = net.W1xTS, C = H, r0 = 32 * idx;
+  }
+  // LDS-DMA of chunk idx into ring slot idx & 1: wave-instruction w writes LDS granules
+  // [64 w, 64 w + 64) lane-linearly; lane i's source is the granule that belongs there.
+  __device__ __forceinline__ void issue(int idx, uint32_t* ring) const {
+    if (idx >= total) return;
+    const uint32_t* g;
+    int C, r0;
+    desc(idx, g, C, r0);
+    uint32_t* dst = ring + (idx & 1) * (32 * HMAX);
+    const int gpr = C >> 2, m = split_swz(C), lane = threadIdx.x & 63;
+    for (int w = threadIdx.x >> 6; w < (C >> 3); w += NTH / 64) {
+      const int G = 64 * w + lane, r = G / gpr, gs = (G - r * gpr) ^ (r & m);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(g + (size_t)(r0 + r) * C + 4 * gs),
+          (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+    }
+  }
+  // One barrier per chunk: it retires this wave's DMA of chunk idx (vmcnt(0) before s_barrier)
+  // and every wave's reads of chunk idx - 1, whose slot then receives chunk idx + 1.
+  __device__ __forceinline__ const uint32_t* enter(int idx, uint32_t* ring, int& C) const {
+    const uint32_t* g;
+    int r0;
+    desc(idx, g, C, r0);
+    __syncthreads();
+    issue(idx + 1, ring);
+    return ring + (idx & 1) * (32 * HMAX);
+  }
+};
+
+// mlp_tile on the fp16-split MFMA (H % 32 == 0): same inputs, outputs and tile layout; each
+// 16x16x4 f32 chain becomes 16x16x32 f16 chunks (3 MFMAs per 32-wide chunk instead of 8), the
+// weights come pre-split from NetDev::*S, the activations are split in registers.
+template <int KIND, int H, int L, class SH>
+__device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net, SH& sh, float& u_out,
+                                               float& gsum_out, float& gA_out, float& gB_out) {
+  static_assert(H % 32 == 0, "split MLP needs H % 32 == 0");
+  constexpr int HT = H / 16, NU = H / 32;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  uint32_t* wsh = reinterpret_cast<uint32_t*>(sh.W);
+  SplitStream<H, L> ss(net, Eq<KIND>::GRAD_FULL);
+  const int nu1 = ss.C1 >> 5;
+  int chunk = 0;
+  ss.issue(0, wsh);
+  float act[L][HT][4];
+  half8 bh[NU], bl[NU];
+
+  // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+  half8 xh[NXP_MAX / 32], xl[NXP_MAX / 32];  // the noise tile as B operand, split once
+#pragma unroll
+  for (int u = 0; u < NXP_MAX / 32; ++u) {
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = u < nu1 ? sh.S[(32 * u + 4 * qq + (j & 3) + 16 * (j >> 2)) * SS + pp] : 0.f;
+    split8(x, xh[u], xl[u]);
+  }
+#pragma unroll
+  for (int T0 = 0; T0 < HT; T0 += 2) {
+    int C;
+    const uint32_t* wch = ss.enter(chunk++, wsh, C);
+    floatx4 am[2], ac[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NXP_MAX / 32; ++u) {
+      if (u < nu1) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          half8 ah, al;
+          load_a_split(wch, C, 16 * t + jj, u, qq, ah, al);
+          am[t] = mfma16(ah, xh[u], am[t]);
+          ac[t] = mfma16(ah, xl[u], ac[t]);
+          ac[t] = mfma16(al, xh[u], ac[t]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * (T0 + t) + 4 * qq + r;
+        const float acc = fmaf(ac[t][r], SPLIT_INV, am[t][r]);
+        act[0][T0 + t][r] = elu(fmaf(cm, acc, fmaf(sh.vec[H + h], tau, sh.vec[h])));
+      }
+  }
+  // ---------------- hidden layers
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[l - 1][2 * u], act[l - 1][2 * u + 1], bh[u], bl[u]);
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
+      floatx4 o[2];
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = elu(o[t][r] + sh.bh[l * H + 16 * (T0 + t) + 4 * qq + r]);
+    }
+  }
+  // ---------------- output u = wout . a_L + bout ; delta_L = wout * elu'(a_L)
+  float up = 0.f;
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      const float w = sh.vec[2 * H + h];
+      up = fmaf(w, act[L - 1][T][r], up);
+      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+    }
+  u_out = qsum(up) + net.bout;
+  // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[l + 1][2 * u], act[l + 1][2 * u + 1], bh[u], bl[u]);
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
+      floatx4 o[2];
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = o[t][r] * delu_from_a(act[l][T0 + t][r]);
+    }
+  }
+  // ---------------- input gradient
+  if (!Eq<KIND>::GRAD_FULL) {
+    float gp = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp = fmaf(sh.vec[3 * H + 16 * T + 4 * qq + r], act[0][T][r], gp);
+    gsum_out = qsum(gp);
+    gA_out = gB_out = 0.f;
+  } else {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[0][2 * u], act[0][2 * u + 1], bh[u], bl[u]);
+    float A = 0.f, B = 0.f;
+    for (int T0 = 0; T0 < (ss.C1 >> 4); T0 += 2) {
+      int C;
+      const uint32_t* wch = ss.enter(chunk++, wsh, C);
+      floatx4 o[2];
+      split_rows32<NU>(wch, C, jj, qq, bh, bl, o);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = 16 * (T0 + t) + 4 * qq + r;
+          if (d < e.nx) {
+            const float X = fmaf(cm, sh.S[d * SS + pp], sh.xsh[d]);
+            Eq<KIND>::gacc(e, d, X, o[t][r], A, B);
+          }
+        }
+    }
+    gA_out = qsum(A);
+    gB_out = qsum(B);
+    gsum_out = 0.f;
+  }
+}
+
+// LDS of the fully-nonlinear (GBM) path kernel: every weight matrix stays resident for the
+// 100-direction tangent sweep.  H <= 64, L <= 4.
+template <int H>
+struct LdsGbm {
+  static constexpr int WXS = NXP_MAX + 8;  // W1x row stride (WXS/4 = 2 mod 4)
+  static constexpr int WHS = H + 8;        // hidden row stride
+  float S[NXP_MAX * SS];
+  float W1x[H * WXS];
+  float Wh[3][H * WHS];
+  float vec[4 * HMAX];
+  float bh[4 * HMAX];
+  float xsh[NXP_MAX];
+  float hb[NXP_MAX];
+  float gst[4 * P * NSG];
+  float fst[4 * P * NSG];
+  float wx[NSG];
+  float tau[P], cmul[P], bsh[P], fbp[P];
+  float smt[P];                    // Hessian labels: s - t per path
+  unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
+};
+
+__device__ __forceinline__ float d2elu_from_a(float a) { return a > 0.f ? 0.f : a + 1.0f; }
+
+// Diagonal of the x-Hessian of u at (s, X_s) for this wave's 16 paths, contracted with the
+// path's SDGD index histogram: s1 = sum_d cnt[d] u_dd, s2 = sum_d cnt[d] |u_dd|.
+// Uses u_dd = sum_l < lam_l, elu''(z_l) * zdot_l^2 >, with lam_l = du/da_l (one backward pass)
+// and zdot_l = dz_l/dx_d (first-order tangents only): half the MACs of second-order
+// forward mode.  All GEMMs are v_mfma_f32_16x16x4_f32 in the hidden x path orientation.
+template <int H, int L>
+__device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt, float& s1_out,
+                                          float& s2_out) {
+  constexpr int HT = H / 16;
+  constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  float act[L][HT][4];
+  float lam[L][HT][4];
+  // forward
+#pragma unroll
+  for (int T = 0; T < HT; ++T) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    for (int t = 0; t < nxt; ++t) {
+      const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+      const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+      acc = mfma4(a.x, bc[0], acc);
+      acc = mfma4(a.y, bc[SS], acc);
+      acc = mfma4(a.z, bc[2 * SS], acc);
+      acc = mfma4(a.w, bc[3 * SS], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = sh.Wh[l - 1] + (16 * T + jj) * WHS + 4 * qq;
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+        acc = mfma4(a.x, act[l - 1][t][0], acc);
+        acc = mfma4(a.y, act[l - 1][t][1], acc);
+        acc = mfma4(a.z, act[l - 1][t][2], acc);
+        acc = mfma4(a.w, act[l - 1][t][3], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+    }
+  }
+  // adjoints lam_l = du/da_l
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lam[L - 1][T][r] = sh.vec[2 * H + 16 * T + 4 * qq + r];
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+    float Bm[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l + 1][t][r]) * lam[l + 1][t][r];
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)  // A[i][k] = W_{l+1}[k][i]: column 16T+jj, row 16t+4qq+r
+          acc = mfma4(sh.Wh[l][(16 * t + 4 * qq + r) * WHS + 16 * T + jj], Bm[t][r], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lam[l][T][r] = acc[r];
+    }
+  }
+  // tangent sweep over the state dimensions
+  float s1 = 0.f, s2 = 0.f;
+  for (int d = 0; d < e.nx; ++d) {
+    float z[HT][4];
+    float term = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+        term = fmaf(lam[0][T][r] * d2elu_from_a(act[0][T][r]), z[T][r] * z[T][r], term);
+      }
+#pragma unroll
+    for (int l = 1; l < L; ++l) {
+      float Bm[HT][4];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l - 1][t][r]) * z[t][r];
+#pragma unroll
+      for (int T = 0; T < HT; ++T) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* wrow = sh.Wh[l - 1] + (16 * T + jj) * WHS + 4 * qq;
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+          acc = mfma4(a.x, Bm[t][0], acc);
+          acc = mfma4(a.y, Bm[t][1], acc);
+          acc = mfma4(a.z, Bm[t][2], acc);
+          acc = mfma4(a.w, Bm[t][3], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          z[T][r] = acc[r];
+          term = fmaf(lam[l][T][r] * d2elu_from_a(act[l][T][r]), acc[r] * acc[r], term);
+        }
+      }
+    }
+    const float ud = qsum(term);
+    const float c = (float)sh.cnt[d * P + pp];
+    s1 = fmaf(c, ud, s1);
+    s2 = fmaf(c, fabsf(ud), s2);
+  }
+  s1_out = s1;
+  s2_out = s2;
+}
+
+// ------------------------------------------------------------------------------ kernels
+// Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
+template <int KIND>
+__global__ void k_sample_points(EqDev e, int n, uint32_t k0, uint32_t k1, uint32_t c3t, uint32_t c3x0,
+                                uint32_t c3x, uint32_t point_base, float eps, float alpha_init_sqrt, float* tx) {
+  const int nb = (e.nx + 3) >> 2;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = gid / nb, j = gid - i * nb;
+  if (i >= n) return;
+  const uint32_t ig = point_base + (uint32_t)i;
+  const float U = u01_co(philox4x32_10(0u, 0u, ig, c3t, k0, k1).x);
+  const float t = (e.T - 2.f * eps) * (1.f - U) + eps;
+  float* row = tx + (size_t)i * (1 + e.nx);
+  if (j == 0) row[0] = t;
+  const f4 z = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x, k0, k1));
+  f4 z0 = {0.f, 0.f, 0.f, 0.f};
+  if (KIND == DPI_EQ_OU) {
+    z0 = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x0, k0, k1));
+    z0.a *= alpha_init_sqrt;
+    z0.b *= alpha_init_sqrt;
+    z0.c *= alpha_init_sqrt;
+    z0.d *= alpha_init_sqrt;
+  }
+  const float sc = sqrtf(t) * e.asq;
+  const float zz[4] = {z.a, z.b, z.c, z.d};
+  const float xx[4] = {z0.a, z0.b, z0.c, z0.d};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int d = 4 * j + q;
+    if (d < e.nx) row[1 + d] = fmaf(sc, zz[q], xx[q]);
+  }
+}
+
+// Block-wide sum over 256 threads (result on every thread); red: >= 4 floats of LDS.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+constexpr int NTHB = 1024;  // baseline workgroup: 16 waves
+__device__ __forceinline__ float block_sum_b(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float a = 0.f;
+  for (int w = 0; w < NTHB / 64; ++w) a += red[w];
+  return a;
+}
+
+// Baseline per point (one workgroup per point): g(x), the state-dependent part of
+// f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
+// f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
+// over k-slices (weights read coalesced through the transposed copies), no LDS staging.
+template <int KIND, bool ZERO>
+__global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
+                                                  float* __restrict__ gx, float* __restrict__ fb,
+                                                  float* __restrict__ bx, float* __restrict__ hb) {
+  __shared__ float xs[NXP_MAX];
+  __shared__ float act[4][HMAX];
+  __shared__ float dbuf[2][HMAX];
+  __shared__ float red[NTHB / 64];
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int nx = e.nx, F = 1 + nx;
+  const float* row = tx + (size_t)i * F;
+  const float t = row[0];
+  for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
+  __syncthreads();
+  // g(x): per-thread dims, then per-statistic block sums in fixed order (one barrier pair)
+  {
+    __shared__ float redn[NTHB / 64][NSG];
+    float st[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = 0.f;
+    for (int d = tid; d < nx; d += NTHB) Eq<KIND>::gstat(e, d, xs[d], st);
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = wave_sum(st[c]);
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) redn[tid >> 6][c] = st[c];
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float a = 0.f;
+        for (int w = 0; w < NTHB / 64; ++w) a += redn[w][c];
+        st[c] = a;
+      }
+      gx[i] = Eq<KIND>::gfin(e, st);
+    }
+  }
+  float Cb = 0.f;
+  if constexpr (KIND == DPI_EQ_GBM) {
+    // exact-solution part of ffi at (t, x) (equations.py:457-466)
+    float arg[NSG], sn[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      float v = 0.f;
+      if (c < e.nodes)
+        for (int d = tid; d < nx; d += NTHB) v = fmaf(e.gw[c * F + 1 + d], xs[d], v);
+      v = block_sum_b(v, red);
+      arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, v) : 0.f;
+      sn[c] = __sinf(arg[c]);
+    }
+    const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
+    Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+    if (ZERO) {
+      for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
+      if (tid == 0) fb[i] = Cb;
+      return;
+    }
+  }
+  if (ZERO) {
+    if (tid == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int H = net.H, L = net.L, nxp = net.nxp;
+  // Mat-vecs y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), coalesced in h): thread tid takes
+  // unit h = tid % H and the k-slice tid / H of NTHB / H slices (<= 16 values, all loads issued
+  // before the first FMA: one memory latency per layer); the slices are added in fixed order by
+  // the unit's owner.
+  __shared__ float part[NTHB];
+  auto matvec = [&](const float* __restrict__ Wt, const float* v, int K) -> float {
+    const int h = tid % H, ns = NTHB / H, sl = tid / H;
+    const int kc = (K + ns - 1) / ns, k0 = sl * kc, k1 = min(K, k0 + kc);  // kc <= 16
+    float w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = k0 + j < k1 ? Wt[(size_t)(k0 + j) * H + h] : 0.f;  // all loads in flight
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      if (k0 + j < k1) a0 = fmaf(w[j], v[k0 + j], a0);
+      if (k0 + j + 1 < k1) a1 = fmaf(w[j + 1], v[k0 + j + 1], a1);
+    }
+    part[tid] = a0 + a1;
+    __syncthreads();
+    float y = 0.f;
+    if (tid < H)
+      for (int j = 0; j < ns; ++j) y += part[j * H + tid];
+    return y;  // valid for tid < H; the caller's barrier precedes the next use of part
+  };
+  // layer 1
+  {
+    const float acc = matvec(net.W1xT, xs, nx);
+    if (tid < H) {
+      bx[(size_t)i * H + tid] = net.b1[tid] + acc;
+      act[0][tid] = elu(fmaf(net.w1t[tid], t, net.b1[tid] + acc));
+    }
+    __syncthreads();
+  }
+  for (int l = 1; l < L; ++l) {
+    const float acc = matvec(net.WT[l], act[l - 1], H);
+    if (tid < H) act[l][tid] = elu(acc + net.b[l][tid]);
+    __syncthreads();
+  }
+  if constexpr (KIND == DPI_EQ_GBM) {
+    // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
+    // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
+    __shared__ float lamb[4][HMAX];
+    __shared__ float ztb[2][64][NXP_MAX];
+    if (tid < H) lamb[L - 1][tid] = net.wout[tid];
+    __syncthreads();
+    for (int l = L - 2; l >= 0; --l) {
+      if (tid < H) {
+        const float* w = net.W[l + 1];
+        float acc = 0.f;
+        for (int h = 0; h < H; ++h) acc = fmaf(w[(size_t)h * H + tid], delu_from_a(act[l + 1][h]) * lamb[l + 1][h], acc);
+        lamb[l][tid] = acc;
+      }
+      __syncthreads();
+    }
+    // Tangent sweep as an LDS mat-mat per layer: thread (d = tid % 128, hg = tid / 128) owns the
+    // rows h = hg, hg + 8, ... of the tangent Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k]) Z_{l-1}[k][d].
+    __shared__ float wsc[64 * 65];
+    __shared__ float udp[8][NXP_MAX];
+    const int d = tid % NXP_MAX, hg = tid / NXP_MAX;  // NTHB = 8 x NXP_MAX
+    float ud = 0.f;
+    for (int h = hg; h < H; h += 8) {
+      const float z = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
+      ztb[0][h][d] = z;
+      ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
+    }
+    int cz = 0;
+    for (int l = 1; l < L; ++l) {
+      for (int q = tid; q < H * H; q += NTHB) {
+        const int h = q / H, k = q - h * H;
+        wsc[h * 65 + k] = net.W[l][q] * delu_from_a(act[l - 1][k]);
+      }
+      __syncthreads();  // wsc and Z_{l-1} complete
+      for (int h = hg; h < H; h += 8) {
+        float z = 0.f;
+        for (int k = 0; k < H; ++k) z = fmaf(wsc[h * 65 + k], ztb[cz][k][d], z);
+        ztb[cz ^ 1][h][d] = z;
+        ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z * z, ud);
+      }
+      cz ^= 1;
+      __syncthreads();  // before wsc is overwritten
+    }
+    udp[hg][d] = ud;
+    __syncthreads();
+    if (tid < NXP_MAX) {
+      float a = 0.f;
+      for (int g = 0; g < 8; ++g) a += udp[g][tid];
+      hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
+    }
+    if (tid == 0) fb[i] = Cb;
+    return;
+  }
+  const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
+  int cur = 0;
+  if (tid < H) dbuf[0][tid] = net.wout[tid] * delu_from_a(act[L - 1][tid]);
+  __syncthreads();
+  for (int l = L - 2; l >= 0; --l) {
+    // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
+    const float acc = matvec(net.W[l + 1], dbuf[cur], H);
+    if (tid < H) dbuf[cur ^ 1][tid] = acc * delu_from_a(act[l][tid]);
+    cur ^= 1;
+    __syncthreads();
+  }
+  float gs = 0.f, gA = 0.f, gB = 0.f;
+  if (!Eq<KIND>::GRAD_FULL) {
+    gs = block_sum_b(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
+  } else {
+    float A = 0.f, B = 0.f;
+    for (int d = tid; d < nx; d += NTHB) {
+      float z = 0.f;
+      for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], dbuf[cur][k], z);
+      Eq<KIND>::gacc(e, d, xs[d], z, A, B);
+    }
+    gA = block_sum_b(A, red);
+    gB = block_sum_b(B, red);
+  }
+  if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
+}
+
+struct PathArgs {
+  const float* tx;
+  const float* gx;
+  const float* fb;
+  const float* bx;
+  const float* hb;  // GBM: baseline Hessian diagonal [n][NXP_MAX]
+  float* partial;
+  int n, nbp, m_begin, K, flags;
+  uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
+  int order;  // phase order policy (k_paths)
+  int split;  // fused MLP on the fp16-split MFMA
+  float* hpart;            // Hessian labels: block sums [n][nbp][nx*nx]
+  uint32_t c3h1, c3h2;     // Hessian labels: Malliavin normal streams (tags HTERM, HINT)
+};
+
+// ------------------------------------------------------------------------------ Hessian labels
+// Malliavin-weight Hessian block of generate_with_gradients_and_hessians (picard/data.py:1220-1223;
+// terminal :1185-1199, integral :869-881), per 64-path block, after phase 3 of k_paths:
+//   H_blk = sum_p [ aI_p (N2 N2^T - I) + aT_p (N1 N1^T - I) ]
+//   aI = (T-t) (f(s, x + a sqrt(s-t) N2) + f(s, x - ...) - 2 f_b) / 2 / (s-t)     (full Hessian f)
+//   aT = (g(x + a sqrt(T-t) N1) + g(x - ...) - 2 g(x)) / 2 / (T-t)
+// N1, N2: fresh normals (tags HTERM / HINT, k = 0), written into the noise tile in turn; the
+// outer-product sums are (nx x 64) (64 x nx) products on v_mfma_f32_16x16x4_f32 over the upper
+// triangle of 16 x 16 tiles (wave w owns tiles w, w+4, ...), mirrored on store.
+template <int H, int L>
+__device__ __forceinline__ void hess_accum(LdsGbm<H>& sh, const float* wgt, int NT, floatx4 (&acc)[9]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, jj = lane & 15, qq = lane >> 4;
+  const int ntiles = NT * (NT + 1) / 2;
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) {
+    const int q = wv + 4 * sl;
+    if (q < ntiles) {
+      int I = 0, r = q;
+      while (r >= NT - I) {
+        r -= NT - I;
+        ++I;
+      }
+      const int J = I + r;
+      const float* ra = sh.S + (16 * I + jj) * SS + qq;
+      const float* rb = sh.S + (16 * J + jj) * SS + qq;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) acc[sl] = mfma4(ra[4 * t] * wgt[4 * t + qq], rb[4 * t], acc[sl]);
+    }
+  }
+}
+
+template <int KIND, int H, int L, bool ZERO>
+__device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, const PathArgs& a, LdsGbm<H>& sh,
+                                           int i, int blk, uint32_t ig, uint32_t m, float s, float smt, float tmt,
+                                           float g_x, int nxp) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
+  const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2, NT = nxp / 16;
+  // f at (s, x + cmul S) with the full Hessian diagonal (get_f without SDGD, data.py:1262-1272);
+  // valid in the lanes of group qq == 0 for path pp
+  auto f_eval = [&]() -> float {
+    float s1 = 0.f, s2 = 0.f;
+    if (!ZERO) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+    const float c1 = 0.5f * (1.0f - e.alpha), c2 = 0.25f;
+    float arg[NSG], sn[NSG];
+    const float spp = sh.tau[pp], cpp = sh.cmul[pp];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      arg[c] = 0.f;
+      if (c < e.nodes) {
+        const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
+                          sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
+        arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+      }
+      sn[c] = __sinf(arg[c]);
+    }
+    const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
+    return c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+  };
+  float* wgt = sh.bsh;  // per-path weights of the current outer-product term
+  floatx4 acc[9];
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) acc[sl] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- integral term: N2 -> noise tile, w . N2 for the exact-solution terms
+  __syncthreads();  // phase 3 is done with the integral noise tile
+  {
+    float fs[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) fs[c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = wv + 4 * c;
+      if (j < nb) {
+        const f4 z = normals4(philox4x32_10((uint32_t)j, m, ig, a.c3h2, a.k0, a.k1));
+        const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          const float v = d < nx ? zz[q] : 0.f;
+          sh.S[d * SS + lane] = v;
+          if (d < nx)
+#pragma unroll
+            for (int c2 = 0; c2 < NSG; ++c2)
+              if (c2 < e.nodes) fs[c2] = fmaf(e.gw[c2 * F + 1 + d], v, fs[c2]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fs[c];
+  }
+  const float cw = e.asq * sqrtf(smt);
+  if (wv == 0) {
+    sh.cmul[lane] = cw;
+    sh.smt[lane] = smt;
+  }
+  __syncthreads();
+  const float fplus = f_eval();
+  __syncthreads();
+  if (wv == 0) sh.cmul[lane] = -cw;
+  __syncthreads();
+  const float fminus = f_eval();
+  const float fbp = sh.fbp[pp];
+  if (qq == 0) wgt[pp] = tmt * ((fplus + fminus - 2.f * fbp) * 0.5f / sh.smt[pp]);  // path pp, not this lane's
+  __syncthreads();
+  const float aI = wgt[lane];  // lane = path
+  hess_accum<H, L>(sh, wgt, NT, acc);
+
+  // ---- terminal term: N1 -> noise tile, g(x +- a sqrt(T-t) N1)
+  __syncthreads();  // every wave is done reading N2 and the weights
+  float gp[NSG], gm[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) gp[c] = gm[c] = 0.f;
+  const float cw1 = e.asq * sqrtf(tmt);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int j = wv + 4 * c;
+    if (j < nb) {
+      const f4 z = normals4(philox4x32_10((uint32_t)j, m, ig, a.c3h1, a.k0, a.k1));
+      const float zz[4] = {z.a, z.b, z.c, z.d};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        const float v = d < nx ? zz[q] : 0.f;
+        sh.S[d * SS + lane] = v;
+        if (d < nx) {
+          Eq<KIND>::gstat(e, d, fmaf(cw1, v, sh.xsh[d]), gp);
+          Eq<KIND>::gstat(e, d, fmaf(-cw1, v, sh.xsh[d]), gm);
+        }
+      }
+    }
+  }
+  auto wave_stats = [&](float (&st)[NSG]) -> float {  // g from the 4 waves' partial statistics
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = st[c];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      st[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
+               sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
+    __syncthreads();
+    return Eq<KIND>::gfin(e, st);
+  };
+  const float gplus = wave_stats(gp);
+  const float gminus = wave_stats(gm);
+  const float aT = (gplus + gminus - 2.f * g_x) * 0.5f / tmt;
+  if (wv == 0) wgt[lane] = aT;
+  __syncthreads();
+  hess_accum<H, L>(sh, wgt, NT, acc);
+
+  // ---- identity part, store (upper tiles mirrored)
+  const float dsum = wave_sum(aI + aT);
+  float* out = a.hpart + ((size_t)i * a.nbp + blk) * (size_t)nx * nx;
+  const int ntiles = NT * (NT + 1) / 2;
+#pragma unroll
+  for (int sl = 0; sl < 9; ++sl) {
+    const int q = wv + 4 * sl;
+    if (q < ntiles) {
+      int I = 0, r = q;
+      while (r >= NT - I) {
+        r -= NT - I;
+        ++I;
+      }
+      const int J = I + r;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int d1 = 16 * I + 4 * qq + rr, d2 = 16 * J + jj;
+        if (d1 < nx && d2 < nx && d1 <= d2) {  // upper triangle, mirrored: exactly symmetric labels
+          const float v = acc[sl][rr] - (d1 == d2 ? dsum : 0.f);
+          out[(size_t)d1 * nx + d2] = v;
+          if (d1 != d2) out[(size_t)d2 * nx + d1] = v;
+        }
+      }
+    }
+  }
+}
+
+// One workgroup = (point i, 64 consecutive MC indices).  See the file header.
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false>
+__global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+  static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
+  constexpr bool GBM = KIND == DPI_EQ_GBM;
+  using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
+  __shared__ SH sh;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = blockIdx.x / a.nbp, blk = blockIdx.x - i * a.nbp;
+  const uint32_t ig = a.point_base + (uint32_t)i;
+  const uint32_t m = (uint32_t)(a.m_begin + P * blk + lane);
+  const int nx = e.nx, F = 1 + nx;
+  const int nb = (nx + 3) >> 2;
+  const int nxp = ZERO ? ((nx + 15) & ~15) : net.nxp;
+  const bool TERM = a.flags & DPI_TERMINAL, INTG = a.flags & DPI_INTEGRAL;
+  const float* txr = a.tx + (size_t)i * F;
+  const float t = txr[0];
+  const float tmt = e.T - t;
+  const float g_x = a.gx[i], f_b = a.fb[i];
+  const float Kf = (float)a.K;
+
+  for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
+  const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
+  for (int idx = tid; idx < (nxpz - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
+    const int d = 4 * nb + idx / P, p = idx % P;
+    sh.S[d * SS + p] = 0.f;
+  }
+  if (!ZERO) {
+    for (int h = tid; h < H; h += NTH) {
+      sh.vec[h] = a.bx[(size_t)i * H + h];  // b1 + W1x x (from k_baseline)
+      sh.vec[H + h] = net.w1t[h];
+      sh.vec[2 * H + h] = net.wout[h];
+      sh.vec[3 * H + h] = net.c1[h];
+    }
+    for (int l = 1; l < L; ++l)
+      for (int h = tid; h < H; h += NTH) sh.bh[l * H + h] = net.b[l][h];
+  }
+  if constexpr (GBM) {
+    if (!ZERO) {  // all weights resident for the tangent sweep
+      constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+      for (int idx = tid; idx < H * nxp; idx += NTH) {
+        const int h = idx / nxp, d = idx - h * nxp;
+        sh.W1x[h * WXS + d] = net.W1x[idx];
+      }
+      for (int l = 1; l < L; ++l)
+        for (int idx = tid; idx < H * H; idx += NTH) {
+          const int h = idx / H, k = idx - h * H;
+          sh.Wh[l - 1][h * WHS + k] = net.W[l][idx];
+        }
+    }
+    for (int d = tid; d < nxp; d += NTH) sh.hb[d] = d < nx ? a.hb[(size_t)i * NXP_MAX + d] : 0.f;
+    for (int idx = tid; idx < nxp * P / 4; idx += NTH) reinterpret_cast<uint32_t*>(sh.cnt)[idx] = 0u;
+    if (wv == 0) {  // w_k . x for this point
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float v = 0.f;
+        if (c < e.nodes)
+          for (int d = lane; d < nx; d += 64) v = fmaf(e.gw[c * F + 1 + d], txr[1 + d], v);
+        v = wave_sum(v);
+        if (lane == 0) sh.wx[c] = v;
+      }
+    }
+  }
+  // s ~ U(t, T] for this lane's path (data.py:359); integral/terminal step multipliers
+  const float U = u01_oc(philox4x32_10(0u, m, ig, a.c3s, a.k0, a.k1).x);
+  // Hessian labels: s = U (T - t) + t + 1e-4 (data.py:848) and Y without the first-order
+  // terminal estimator's extra 1/sqrt(alpha) (data.py:1175-1178, :851-864)
+  const float smt = U * tmt + (HESS ? 1e-4f : 0.f);  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
+  const float s = HESS ? t + smt : fmaf(U, tmt, t);
+  const float ya = HESS ? 1.f : e.asq;
+  const float cI = e.asq * sqrtf(smt / Kf);            // X_s = x + cI * sum_k xi_k
+  const float yI = 1.0f / (sqrtf(Kf * smt) * ya);      // Y_s = yI * sum_k xi_k   (data.py:520)
+  const float cT = e.asq * sqrtf(tmt / Kf);
+  const float yT = 1.0f / (sqrtf(Kf * tmt) * ya);      // Y_T (data.py:917)
+  if (wv == 0) {
+    sh.tau[lane] = s;
+    sh.cmul[lane] = cI;
+  }
+  __syncthreads();  // xsh ready
+
+  // ---------------- phase 1: K-step Euler–Maruyama rollouts
+  float ST[8][4];
+  float gst[NSG], fst[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) gst[c] = fst[c] = 0.f;
+  if constexpr (GBM) {
+    // SDGD indices (data.py:497-502): v draws in [0, nx) with replacement -> histogram cnt[d][path]
+    if (INTG && wv == 1) {  // one wave owns the histogram (wave 1 has 12 rollout blocks, not 13)
+      if (e.sdgd_v > 0) {
+        for (int q0 = 0; q0 < e.sdgd_v; q0 += 4) {
+          const u32x4 w = philox4x32_10((uint32_t)(q0 >> 2), m, ig, a.c3q, a.k0, a.k1);
+          const uint32_t ws4[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (q0 + r < e.sdgd_v) {
+              const int idx = (int)(((uint64_t)ws4[r] * (uint32_t)nx) >> 32);
+              sh.cnt[idx * P + lane] += 1;
+            }
+        }
+      } else {
+        for (int d = 0; d < nx; ++d) sh.cnt[d * P + lane] = 1;  // exact diagonal: every d once
+      }
+    }
+  }
+  auto terminal_rollout = [&]() {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = wv + 4 * c;  // terminal dim-blocks of this wave
+      ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
+      if (TERM && j < nb) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        for (int k = 0; k < a.K; ++k) {
+          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
+          s0 += z.a;
+          s1 += z.b;
+          s2 += z.c;
+          s3 += z.d;
+        }
+        ST[c][0] = s0 * BM_SCALE;
+        ST[c][1] = s1 * BM_SCALE;
+        ST[c][2] = s2 * BM_SCALE;
+        ST[c][3] = s3 * BM_SCALE;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          if (d < nx) Eq<KIND>::gstat(e, d, fmaf(cT, ST[c][q], sh.xsh[d]), gst);
+        }
+      }
+    }
+  };
+  auto integral_rollout = [&]() {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
+      if (j < nb) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        if (INTG) {
+          for (int k = 0; k < a.K; ++k) {
+            const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
+            s0 += z.a;
+            s1 += z.b;
+            s2 += z.c;
+            s3 += z.d;
+          }
+        }
+        const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          sh.S[d * SS + lane] = d < nx ? sv[q] : 0.f;
+          if constexpr (GBM) {  // w_k . S for the exact-solution terms at X_s = x + cI S
+            if (d < nx) {
+#pragma unroll
+              for (int c = 0; c < NSG; ++c)
+                if (c < e.nodes) fst[c] = fmaf(e.gw[c * F + 1 + d], sv[q], fst[c]);
+            }
+          }
+        }
+      }
+    }
+  };
+  // g(X_T) statistics over the 4 waves in fixed order; the barrier also publishes S / fst
+  auto terminal_finish = [&]() -> float {
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) sh.gst[(wv * P + lane) * NSG + c] = gst[c];
+    if constexpr (GBM) {
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) sh.fst[(wv * P + lane) * NSG + c] = fst[c];
+    }
+    __syncthreads();
+    float gT = 0.f;
+    if (TERM) {
+#pragma unroll
+      for (int c = 0; c < NSG; ++c)
+        gst[c] = ((sh.gst[(0 * P + lane) * NSG + c] + sh.gst[(1 * P + lane) * NSG + c]) +
+                  sh.gst[(2 * P + lane) * NSG + c]) + sh.gst[(3 * P + lane) * NSG + c];
+      gT = Eq<KIND>::gfin(e, gst);
+    }
+    return TERM ? gT - g_x : 0.f;  // (g(X_T) - g(x)) (data.py:923)
+  };
+
+  // ---------------- phase 2: u, grad u (or the SDGD Hessian diagonal) at (s, X_s) and f -> bsh
+  auto integrand = [&]() {
+    if constexpr (!GBM) {
+      float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
+      if (!ZERO && INTG) {
+        if constexpr (SPLIT)
+          mlp_tile_split<KIND, H, L>(e, net, sh, u, gs, gA, gB);
+        else
+          mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
+      }
+      const int pp = 16 * wv + (lane & 15);
+      if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
+    } else {
+      // ffi (equations.py:457-466) with u_ii from SDGD (data.py:1273-1303); the baseline f_b
+      // gathers the point's Hessian diagonal at this path's indices (data.py:1293-1302).
+      const int jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
+      float s1 = 0.f, s2 = 0.f;
+      if (!ZERO && INTG) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+      const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
+      const float c1 = 0.5f * (1.0f - e.alpha) * (float)nx / vv, c2 = 0.25f * (float)nx / vv;
+      float arg[NSG], sn[NSG];
+      const float spp = sh.tau[pp], cpp = sh.cmul[pp];
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        arg[c] = 0.f;
+        if (c < e.nodes) {
+          const float ws = ((sh.fst[(0 * P + pp) * NSG + c] + sh.fst[(1 * P + pp) * NSG + c]) +
+                            sh.fst[(2 * P + pp) * NSG + c]) + sh.fst[(3 * P + pp) * NSG + c];
+          arg[c] = fmaf(e.gw[c * F], spp, fmaf(cpp, ws, sh.wx[c]));
+        }
+        sn[c] = __sinf(arg[c]);
+      }
+      const float ah = qsum(Eq<KIND>::abs_hess_partial(e, sn, qq, 4));
+      float b1 = 0.f, b2 = 0.f;  // baseline Hessian diagonal gathered at this path's indices
+      for (int d = qq; d < nx; d += 4) {
+        const float c = (float)sh.cnt[d * P + pp], h = sh.hb[d];
+        b1 = fmaf(c, h, b1);
+        b2 = fmaf(c, fabsf(h), b2);
+      }
+      b1 = qsum(b1);
+      b2 = qsum(b2);
+      const float f = c1 * s1 + c2 * s2 + Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+      const float fbp = f_b + c1 * b1 + c2 * b2;
+      if (qq == 0) {
+        sh.bsh[pp] = INTG ? tmt * (f - fbp) : 0.f;
+        sh.fbp[pp] = fbp;
+      }
+    }
+  };
+
+  // Phase order.  Two workgroups share a CU; if both run their MFMA phase at the same time the
+  // matrix pipe idles during the (longer) VALU rollouts.  Workgroups on the "terminal last"
+  // order run the MLP between the integral and the terminal rollout, so a co-resident pair in
+  // opposite orders overlaps one's MFMA phase with the other's VALU phase.  The results do not
+  // depend on the order (same counters, same per-lane arithmetic).
+  bool tlast = false;
+  if constexpr (SPLIT) {
+    tlast = true;  // measured faster, and the terminal sums are not live across the MLP (no spills)
+  } else if constexpr (!GBM) {
+    if (a.order == 1) tlast = (__builtin_amdgcn_s_getreg((3 << 11) | (16 << 6) | 4) & 1) != 0;  // HW_ID.TG_ID
+    else if (a.order == 2) tlast = (blockIdx.x & 1) != 0;
+    else if (a.order == 3) tlast = ((blockIdx.x >> 8) & 1) != 0;
+    else if (a.order == 4) tlast = true;
+  }
+  float ap;
+  if (!tlast) {
+    terminal_rollout();
+    integral_rollout();
+    ap = terminal_finish();
+    integrand();
+    __syncthreads();
+  } else {
+    integral_rollout();
+    __syncthreads();
+    integrand();
+    terminal_rollout();
+    ap = terminal_finish();  // its barrier also publishes bsh
+  }
+
+  // ---------------- phase 3: per-path contributions -> per-block partial slab
+  const float bp = sh.bsh[lane];
+  // partial slab layout [point][2F][block]: the reduce kernel reads each column's blocks contiguously
+  float* out = a.partial + (size_t)i * 2 * F * a.nbp + blk;
+  const int nbs = a.nbp;
+  // per-block sums of c and c^2 for this wave's columns: 2 per owned dim (d = 4 (wv + 4c) + q,
+  // column 8c + 2q + {0: sum, 1: sum of squares}) and, on wave 0, the value column (56, 57)
+  const float aY = ap * yT, bY = bp * yI;
+  float col[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) col[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const int j = wv + 4 * c;
+    if (j < nb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        const float v = d < nx ? fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]) : 0.f;
+        col[8 * c + 2 * q] = v;
+        col[8 * c + 2 * q + 1] = v * v;
+      }
+    }
+  }
+  if (wv == 0) {
+    float fbt;
+    if constexpr (GBM)
+      fbt = sh.fbp[lane];
+    else
+      fbt = f_b + Eq<KIND>::ffc(e);
+    const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
+    col[56] = c0;
+    col[57] = c0 * c0;
+  }
+  const float tot = column_sums64(col);
+  {
+    const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
+    const int d = 4 * (wv + 4 * c) + q;
+    if (lane < 56) {
+      if (wv + 4 * c < nb && d < nx) out[(size_t)(sq * F + 1 + d) * nbs] = tot;
+    } else if (wv == 0 && lane < 58) {
+      out[(size_t)(sq * F) * nbs] = tot;
+    }
+  }
+  if (wv + 28 < nb) {  // nx > 112: the eighth dim-block of this wave, one column at a time
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int d = 4 * (wv + 28) + q;
+      if (d < nx) {
+        const float v = fmaf(aY, ST[7][q], bY * sh.S[d * SS + lane]);
+        const float s1 = wave_sum(v), s2 = wave_sum(v * v);
+        if (lane == 0) {
+          out[(size_t)(1 + d) * nbs] = s1;
+          out[(size_t)(F + 1 + d) * nbs] = s2;
+        }
+      }
+    }
+  }
+  if constexpr (HESS) hess_block<KIND, H, L, ZERO>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
+}
+
+}  // namespace dpi

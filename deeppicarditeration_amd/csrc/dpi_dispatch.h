@@ -1,0 +1,98 @@
+// Host-side handles and the (equation, network shape) -> k_paths / k_baseline instantiation
+// dispatch; dispatch<KIND> is instantiated once per equation kind in dpi_paths_{cha,ou,gbm}.hip
+// so the three families compile in parallel.
+#pragma once
+#include "dpi_device.h"
+
+using namespace dpi;
+
+struct dpi_problem_s {
+  EqDev e;
+  float alpha_init_sqrt;
+  std::vector<void*> dev;
+};
+
+struct dpi_net_s {
+  NetDev d;        // d.kind: 0 zero, 1 mlp, 2 PISGradNet
+  NetPisDev pis;
+  void* blob = nullptr;
+  int n_in = 0;
+};
+
+// ---- dispatch over (equation, network shape)
+struct Launch {
+  bool baseline;
+  const float* tx;
+  int n;
+  float *gx, *fb, *bx, *hb;
+  const PathArgs* a;
+  int nblocks;
+  hipStream_t st;
+  bool hess = false;  // k_paths in Hessian-label mode (GBM only)
+};
+
+template <int KIND, int H, int L, bool Z>
+void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if (q.baseline)
+    hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+                       q.bx, q.hb);
+  else if (q.hess) {
+    if constexpr (KIND == DPI_EQ_GBM) {
+      EqDev e2 = p->e;
+      e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
+                         *q.a);
+    }
+  } else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+    if (q.a->split)
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+    else
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+  } else
+    hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+}
+
+template <int KIND>
+bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if (net->d.kind == 0) {
+    do_launch<KIND, 16, 1, true>(p, net, q);
+    return true;
+  }
+  const int H = net->d.H, L = net->d.L;
+  if (q.baseline) {  // the baseline kernel is shape-generic
+    if (KIND == DPI_EQ_GBM && H > 64) return false;
+    do_launch<KIND, 16, 1, false>(p, net, q);
+    return true;
+  }
+  if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
+#define DPI_SHAPE(HH, LL)                      \
+  if (H == HH && L == LL) {                    \
+    do_launch<KIND, HH, LL, false>(p, net, q); \
+    return true;                               \
+  }
+    DPI_SHAPE(64, 3)
+    DPI_SHAPE(64, 2)
+    DPI_SHAPE(32, 2)
+    DPI_SHAPE(32, 3)
+    DPI_SHAPE(16, 1)
+    DPI_SHAPE(16, 2)
+    DPI_SHAPE(16, 3)
+    return false;
+  } else {
+    DPI_SHAPE(128, 4)
+    DPI_SHAPE(128, 3)
+    DPI_SHAPE(128, 2)
+    DPI_SHAPE(64, 3)
+    DPI_SHAPE(64, 2)
+    DPI_SHAPE(32, 2)
+    DPI_SHAPE(16, 1)
+    DPI_SHAPE(16, 2)
+    DPI_SHAPE(16, 3)
+#undef DPI_SHAPE
+    return false;
+  }
+}
+
+bool dispatch_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

@@ -139,136 +139,188 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(int M, int N, int K, const f
 namespace dpi {
 
 // ---------------------------------------------------------------------------------------------
-// fp16-split variant: x = hi + 2^-11 lo with hi = fp16(x), lo = fp16((x - hi) 2^11), so
-//     x y = hi_x hi_y + 2^-11 (hi_x lo_y + lo_x hi_y) + O(2^-22 |x y|)
-// — three v_mfma_f32_16x16x32_f16 (16 cycles each, K = 32) replace eight v_mfma_f32_16x16x4_f32
-// (32 cycles, K = 4): 5.3x fewer matrix-pipe cycles at ~2.4e-7 relative error per product, fp32
-// accumulation.  Operands are split once while staging global -> LDS into [row][k] fp16 images
-// (row stride 40 halves) so each MFMA fragment is one ds_read_b128.  Valid while |x| < 65504.
-typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
-typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+// Split-storage GEMM (the PISGradNet pipeline's default): every operand and result lives in HBM
+// already split, x = hi + 2^-11 lo, in the fragment order of mlp_tile_split — per row, chunk u of
+// 32 logical columns is 4 granule pairs (q = 0..3) of 8 hi then 8 lo halves holding columns
+// 32u + 4q + (j & 3) + 16 (j >> 2).  That order is what a lane of group q holds in the 16x16 C
+// layout of n-tiles 2u, 2u+1, so the epilogue stores whole 32-B granule pairs and the next GEMM
+// reads them as MFMA operands with no conversion: the main loop is pure LDS-DMA + ds_read_b128 +
+// v_mfma_f32_16x16x32_f16 (3 per 32-deep product: hi hi + 2^-11 (hi lo + lo hi)).
+//     OUT[m][n] = epi( sum_k W[n][k] X[m][k] ),  m = path (M rows), n = unit (Np, % 32), k (Kp, % 32)
+// W: (Np, Kp) packed split (Kp words per row); X rows at X + m ldx (Kp words); OUT / AUX rows at
+// + m ldc / + m ldaux (Np words).  MFMA A = W tile (rows n), B = X tile (columns m).
+// Block: BM = 256 paths x BN = 32 NT units, 8 waves as 4 (m) x 2 (n), wave tile 64 m x 16 NT n.
+// LDS: a ring of 3 stages of (BN + BM) rows x 128 B (one 32-deep chunk), granules XOR-swizzled
+// by row (g ^ ((r >> 1) & 7)) so the 16 lanes of a ds_read_b128 group hit distinct banks.
+// LDS-DMA runs two chunks ahead: each wave retires its own DMA of chunk u with a counted
+// s_waitcnt vmcnt (the chunk u+1 DMA stays in flight), then a raw s_barrier publishes it — never
+// __syncthreads(), whose vmcnt(0) would drain the ring.  144 KB (NT = 4): 1 block / CU, 2 waves
+// per SIMD.  Blocks are mapped XCD-aware: the n-tiles of one m-tile run back to back on one XCD,
+// so the X tile is fetched from HBM once and re-read from that XCD's L2.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int HBK_ = 32, HLD_ = 40;  // K per stage, LDS row stride in halves
-
-__device__ __forceinline__ void split4(float4 v, half4_t& hi, half4_t& lo) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
+__device__ __forceinline__ float x3_join(uint32_t hw, uint32_t lw, int half) {
+  const _Float16 h = __builtin_bit_cast(_Float16, (uint16_t)(half ? hw >> 16 : hw & 0xFFFFu));
+  const _Float16 l = __builtin_bit_cast(_Float16, (uint16_t)(half ? lw >> 16 : lw & 0xFFFFu));
+  return fmaf((float)l, 1.0f / 2048.0f, (float)h);
+}
+// value of logical column c of a split region starting at word `reg` of a row
+__device__ __forceinline__ float x3_get(const float* row, int reg, int c) {
+  const int u = c >> 5, w = c & 31, q = (w >> 2) & 3, j = (w & 3) + 4 * (w >> 4);
+  const uint32_t* g = reinterpret_cast<const uint32_t*>(row + reg) + 32 * u + 8 * q;
+  return x3_join(g[j >> 1], g[4 + (j >> 1)], j & 1);
+}
+// the 8 values of granule pair (u, q): v[j] = column 32u + 4q + (j & 3) + 16 (j >> 2)
+__device__ __forceinline__ void x3_get8(const float* row, int reg, int u, int q, float (&v)[8]) {
+  const u32x4_t* g = reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint32_t*>(row + reg) + 32 * u + 8 * q);
+  const u32x4_t h = g[0], l = g[1];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const _Float16 h = (_Float16)x[e];
-    hi[e] = h;
-    lo[e] = (_Float16)((x[e] - (float)h) * 2048.0f);
+  for (int j = 0; j < 8; ++j) v[j] = x3_join(h[j >> 1], l[j >> 1], j & 1);
+}
+__device__ __forceinline__ void x3_put8(float* row, int reg, int u, int q, const float (&v)[8]) {
+  u32x4_t h, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t hw = 0, lw = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = v[2 * p + e];
+      const _Float16 hi = (_Float16)x;
+      const _Float16 lo = (_Float16)((x - (float)hi) * 2048.0f);
+      hw |= (uint32_t)__builtin_bit_cast(uint16_t, hi) << (16 * e);
+      lw |= (uint32_t)__builtin_bit_cast(uint16_t, lo) << (16 * e);
+    }
+    h[p] = hw;
+    l[p] = lw;
   }
+  u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(row + reg) + 32 * u + 8 * q);
+  g[0] = h;
+  g[1] = l;
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void k_gemm_nt_f16x3(int M, int N, int K, const float* __restrict__ A, int lda,
-                                                          const float* __restrict__ B, int ldb, float* __restrict__ C,
-                                                          int ldc, const float* __restrict__ bias,
-                                                          const float* __restrict__ aux, int ldaux) {
-  __shared__ _Float16 sm[2][4][GBM_ * HLD_];  // [buf][A hi, A lo, B hi, B lo][row][k]
-  typedef float floatx4_t __attribute__((ext_vector_type(4)));
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int m0 = blockIdx.x * GBM_, n0 = blockIdx.y * GBN_;
-  const int il = lane & 15, ql = lane >> 4;
-  // staging: 128 rows x 32 k = 1024 float4 per operand -> 4 per thread; thread covers k4 = tid & 7
-  const int sk = (tid & 7) * 4, srow = tid >> 3;  // rows srow + 32 h, h = 0..3
-  float4 ra[4], rb[4];
-  auto ld4 = [&](const float* base, int ld, int rows_total, int r, int gk) {
-    float4 v = {0.f, 0.f, 0.f, 0.f};
-    if (r < rows_total) {
-      const float* p = base + (size_t)r * ld + gk;
-      if (gk + 3 < K) {
-        v = *reinterpret_cast<const float4*>(p);
-      } else {
-        if (gk < K) v.x = p[0];
-        if (gk + 1 < K) v.y = p[1];
-        if (gk + 2 < K) v.z = p[2];
-      }
-    }
-    return v;
-  };
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      ra[h] = ld4(A, lda, M, m0 + srow + 32 * h, k0 + sk);
-      rb[h] = ld4(B, ldb, N, n0 + srow + 32 * h, k0 + sk);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int off = (srow + 32 * h) * HLD_ + sk;
-      half4_t hi, lo;
-      split4(ra[h], hi, lo);
-      *reinterpret_cast<half4_t*>(&sm[buf][0][off]) = hi;
-      *reinterpret_cast<half4_t*>(&sm[buf][1][off]) = lo;
-      split4(rb[h], hi, lo);
-      *reinterpret_cast<half4_t*>(&sm[buf][2][off]) = hi;
-      *reinterpret_cast<half4_t*>(&sm[buf][3][off]) = lo;
-    }
-  };
-  floatx4_t hh[4][4], xx[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) hh[a][b] = xx[a][b] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+constexpr int X3_BM = 256, X3_STAGES = 3, X3_THREADS = 512;
 
-  const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int cur = ks & 1;
-    if (ks + 1 < nk) gload((ks + 1) * HBK_);
-    half8_t ah[4], al[4];
+template <int EPI, int NT>
+__global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
+                                                           const float* __restrict__ X, int ldx,
+                                                           float* __restrict__ OUT, int ldc,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ AUX, int ldaux) {
+  static_assert(NT == 2 || NT == 4, "wave n-tiles");
+  constexpr int BN = 32 * NT, BM = X3_BM, STAGE = (BN + BM) * 32, NWAVE = X3_THREADS / 64;
+  constexpr int NINS = (BN + BM) / 8, PER_WAVE = NINS / NWAVE;  // DMA wave-instructions per chunk
+  static_assert(NINS % NWAVE == 0, "DMA instructions split evenly over the waves");
+  __shared__ uint32_t sm[X3_STAGES * STAGE];
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int il = lane & 15, ql = lane >> 4;
+  // XCD-aware bijective remap (dispatch puts block b on XCD b % 8)
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nk = Kp >> 5;
+  const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
+
+  // LDS-DMA of chunk u: wave-instruction w fills rows 8w..8w+7 (128 B each) lane-linearly; lane i
+  // fetches the granule that belongs at slot i & 7 of its row.
+  auto issue = [&](int u) {
+    uint32_t* dst = sm + (u % X3_STAGES) * STAGE;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int off = (wm * 64 + a * 16 + il) * HLD_ + 8 * ql;
-      ah[a] = *reinterpret_cast<const half8_t*>(&sm[cur][0][off]);
-      al[a] = *reinterpret_cast<const half8_t*>(&sm[cur][1][off]);
+    for (int k = 0; k < PER_WAVE; ++k) {
+      const int w = k * NWAVE + wv;
+      const int r = 8 * w + (lane >> 3);
+      const int g = (lane & 7) ^ ((r >> 1) & 7);
+      const uint32_t* src;
+      if (r < BN)
+        src = W + (size_t)(n0 + r) * Kp + 32 * u + 4 * g;
+      else
+        src = Xw + (size_t)min(m0 + r - BN, M - 1) * ldx + 32 * u + 4 * g;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
     }
+  };
+  auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {
+    const int s = (row >> 1) & 7;
+    const uint32_t* rp = buf + row * 32;
+    h = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql) ^ s)));
+    l = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql + 1) ^ s)));
+  };
+
+  f4v hh[NT][4], xx[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) hh[t][b] = xx[t][b] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int u = 0; u < nk; ++u) {
+    // retire this wave's DMA of chunk u (chunk u + 1's PER_WAVE instructions may stay in flight),
+    // then the barrier publishes every wave's part and frees stage (u + 2) % 3 (read in step u - 1)
+    if (u + 1 < nk) {
+      static_assert(PER_WAVE == 6 || PER_WAVE == 5, "vmcnt immediates");
+      if constexpr (PER_WAVE == 6)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < nk) issue(u + 2);
+    const uint32_t* buf = sm + (u % X3_STAGES) * STAGE;
+    h8 ah[NT], al[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) frag(buf, wn * 16 * NT + 16 * t + il, ah[t], al[t]);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const int off = (wn * 64 + b * 16 + il) * HLD_ + 8 * ql;
-      const half8_t bh = *reinterpret_cast<const half8_t*>(&sm[cur][2][off]);
-      const half8_t bl = *reinterpret_cast<const half8_t*>(&sm[cur][3][off]);
+      h8 bh, bl;
+      frag(buf, BN + wm * 64 + 16 * b + il, bh, bl);
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        hh[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh, hh[a][b], 0, 0, 0);
-        xx[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl, xx[a][b], 0, 0, 0);
-        xx[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh, xx[a][b], 0, 0, 0);
+      for (int t = 0; t < NT; ++t) {
+        hh[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t], bh, hh[t][b], 0, 0, 0);
+        xx[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[t], bl, xx[t][b], 0, 0, 0);
+        xx[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[t], bh, xx[t][b], 0, 0, 0);
       }
-    }
-    if (ks + 1 < nk) {  // buffer cur ^ 1 was last read in step ks - 1, which ended in a barrier
-      lstore(cur ^ 1);
-      __syncthreads();
     }
   }
+  // epilogue: lane (il, ql) of m-tile b holds OUT[m = m0 + 64 wm + 16 b + il][n = 16 T + 4 ql + r]
+  // for the wave's n-tiles T; tiles (2c, 2c+1) form granule pair ql of output chunk U.
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int b = 0; b < 4; ++b) {
+    const int m = m0 + wm * 64 + 16 * b + il;
+    if (m >= M) continue;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 64 + b * 16 + il;
-      if (n >= N) continue;
-      const float bn = (EPI == EPI_DELU || bias == nullptr) ? 0.f : bias[n];
+    for (int c = 0; c < NT / 2; ++c) {
+      const int U = (n0 >> 5) + wn * (NT / 2) + c;
+      float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + a * 16 + 4 * ql + r;
-        if (m >= M) continue;
-        float v = fmaf(xx[a][b][r], 1.0f / 2048.0f, hh[a][b][r]);
-        if (EPI == EPI_BIAS) {
-          v += bn;
-        } else if (EPI == EPI_BIAS_ELU) {
-          v += bn;
-          v = v > 0.f ? v : __expf(v) - 1.0f;
-        } else {
-          const float s = aux[(size_t)m * ldaux + n];
-          v *= s > 0.f ? 1.0f : s + 1.0f;
-        }
-        C[(size_t)m * ldc + n] = v;
+        v[r] = fmaf(xx[2 * c][b][r], 1.0f / 2048.0f, hh[2 * c][b][r]);
+        v[4 + r] = fmaf(xx[2 * c + 1][b][r], 1.0f / 2048.0f, hh[2 * c + 1][b][r]);
       }
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
+        if (bias) {
+          const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
+          const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 16 + 4 * ql);
+          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+        }
+        if (EPI == EPI_BIAS_ELU)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+      } else {
+        float a[8];
+        x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
+      }
+      x3_put8(OUT + (size_t)m * ldc, 0, U, ql, v);
     }
+  }
 }
 
 }  // namespace dpi

@@ -35,6 +35,12 @@ struct NetPisDev {
   const float* nn[5];                                 // nn_module weights (h_l x in_l), nn[L] = out (nx x h_L)
   const float* nnb[5];
   const float* nnT[5];                                // transposes for the VJP: nnT[l] = nn[l]^T, nnT[0] = x-part^T
+  // split-storage pipeline (k_gemm_x3): the same matrices packed split, output dims (rows)
+  // zero-padded to multiples of 64 and input dims (columns) to multiples of 32; nnbP = the nn
+  // biases padded alike
+  const uint32_t *te0S, *te2S, *sn0S, *snS[4];
+  const uint32_t *nnS[5], *nnTS[5];
+  const float* nnbP[5];
 };
 
 __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float* out /* stride 1 */, int j) {
@@ -46,14 +52,27 @@ __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float*
   out[PIS_CH + j] = cs;
 }
 
-// Workspace rows of the pipeline (floats per row); every offset a multiple of 4.
+// granule pair (u, q) of the split embedding region: columns c = 32u + 4q + (j & 3) + 16 (j >> 2),
+// sin for c < 64, cos of channel c - 64 above
+__device__ __forceinline__ void pis_embed8(const NetPisDev& pn, float lbd, int u, int q, float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2), ch = c & (PIS_CH - 1);
+    float sn, cs;
+    sincosf(fmaf(pn.coeff[ch], lbd, pn.phase[ch]), &sn, &cs);
+    v[j] = c < PIS_CH ? sn : cs;
+  }
+}
+
+// Workspace rows of the pipeline (floats per row); every offset a multiple of 4 (fp32 storage) or
+// of 32 (split storage, where E/T1/IN/H0/H1/A/NO/D/GX hold split regions and INP = IN's width).
 struct PisRows {
-  int E, T1, IN, H0, H1, A[4], NO, D0, D1, GX, SS, ST, SC, stride;
+  int E, T1, IN, H0, H1, A[4], NO, D0, D1, GX, SS, ST, SC, stride, INP;
 };
 
 // Per-path rollout for the PIS pipeline (phase 1 of k_paths, outputs to global rows).
 // Block = (point, 64-path block) number g0 + blockIdx.x; row r = blockIdx.x * 64 + lane.
-template <int KIND>
+template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                      int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
@@ -61,6 +80,8 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
                                                      float* __restrict__ rows, PisRows L) {
   __shared__ float xsh[NXP_MAX];
   __shared__ float gsts[4 * P * NSG];
+  __shared__ float xs3[X3 ? P * (NXP_MAX + 1) : 1];  // split mode: X_s staged [path][dim]
+  __shared__ float ssh[X3 ? P : 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = g0 + blockIdx.x;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
@@ -118,12 +139,18 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
       const int d = 4 * j + q;
       if (d < nx) {
         row[L.SS + d] = sv[q];
-        row[L.IN + PIS_IN_OFF + d] = fmaf(cI, sv[q], xsh[d]);  // X_s
+        if (X3)
+          xs3[lane * (NXP_MAX + 1) + d] = fmaf(cI, sv[q], xsh[d]);
+        else
+          row[L.IN + PIS_IN_OFF + d] = fmaf(cI, sv[q], xsh[d]);  // X_s
       }
     }
   }
   // time embedding of lambda = T - s (each wave writes 16 of the 64 channels)
-  for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - s, row + L.E, j);
+  if (!X3)
+    for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - s, row + L.E, j);
+  else if (wv == 0)
+    ssh[lane] = s;
 #pragma unroll
   for (int c = 0; c < NSG; ++c) gsts[(wv * P + lane) * NSG + c] = gst[c];
   __syncthreads();
@@ -141,17 +168,57 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
     row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
     row[L.SC + 3] = smt;
   }
+  if constexpr (X3) {  // split rows, whole 32-B granule pairs: X_s -> IN chunks 2.., emb -> E
+    const int nxc = L.INP / 32 - 2;
+    float* rb = rows + (size_t)blockIdx.x * P * L.stride;
+    for (int idx = tid; idx < P * nxc * 4; idx += NTH) {
+      const int p = idx / (nxc * 4), uq = idx - p * (nxc * 4), u = uq >> 2, q = uq & 3;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
+        v[j] = d < nx ? xs3[p * (NXP_MAX + 1) + d] : 0.f;
+      }
+      x3_put8(rb + (size_t)p * L.stride, L.IN, 2 + u, q, v);
+    }
+    for (int idx = tid; idx < P * 16; idx += NTH) {
+      const int p = idx >> 4, u = (idx >> 2) & 3, q = idx & 3;
+      float v[8];
+      pis_embed8(pn, pn.T - ssh[p], u, q, v);
+      x3_put8(rb + (size_t)p * L.stride, L.E, u, q, v);
+    }
+  }
 }
 
 // Baseline rows: IN[i] = [.., x], E[i] = emb(T - t), SC = (t, 1, 0, 0).
+template <bool X3>
 __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx, int n, float* __restrict__ rows,
                              PisRows L) {
   const int i = blockIdx.x, tid = threadIdx.x;
   if (i >= n) return;
   const float* txr = tx + (size_t)i * (1 + nx);
   float* row = rows + (size_t)i * L.stride;
-  for (int d = tid; d < nx; d += blockDim.x) row[L.IN + PIS_IN_OFF + d] = txr[1 + d];
-  for (int j = tid; j < PIS_CH; j += blockDim.x) pis_embed(pn, pn.T - txr[0], row + L.E, j);
+  if constexpr (X3) {
+    const int nxc = L.INP / 32 - 2;
+    for (int idx = tid; idx < nxc * 4; idx += blockDim.x) {
+      const int u = idx >> 2, q = idx & 3;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
+        v[j] = d < nx ? txr[1 + d] : 0.f;
+      }
+      x3_put8(row, L.IN, 2 + u, q, v);
+    }
+    for (int idx = tid; idx < 16; idx += blockDim.x) {
+      float v[8];
+      pis_embed8(pn, pn.T - txr[0], idx >> 2, idx & 3, v);
+      x3_put8(row, L.E, idx >> 2, idx & 3, v);
+    }
+  } else {
+    for (int d = tid; d < nx; d += blockDim.x) row[L.IN + PIS_IN_OFF + d] = txr[1 + d];
+    for (int j = tid; j < PIS_CH; j += blockDim.x) pis_embed(pn, pn.T - txr[0], row + L.E, j);
+  }
   if (tid == 0) {
     row[L.SC + 0] = txr[0];
     row[L.SC + 1] = 1.f;
@@ -161,31 +228,62 @@ __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx,
 }
 
 // grad_x u for one row, reduced into the OU statistics A = sum (X - mu) z, B = sum z^2.
-// 4 threads per row (consecutive lanes), each over dims d = q, q+4, ...
+// 4 threads per row (consecutive lanes, q = 0..3).  fp32 rows: dims d = q, q+4, ...; split rows:
+// the dims of granule pairs (u, q) — d = 32u + 4q + (j & 3) + 16 (j >> 2) — read 32 B at a time.
+template <bool X3>
 __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn, const float* row, const PisRows& L,
                                             float lbd, int q, float& A_out, float& B_out, float& smooth_out) {
   const int nx = e.nx;
   // smooth = smooth_net(emb(lbd))[0] - smooth_net(emb(0))[0]  (solution.py:236-254)
   float sr = 0.f;
-  for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
+  if constexpr (X3) {
+#pragma unroll
+    for (int u = 0; u < PIS_CH / 32; ++u) {
+      float v[8];
+      x3_get8(row, L.H0, u, q, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], v[j], sr);
+    }
+  } else {
+    for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
+  }
   sr += __shfl_xor(sr, 1, 64);
   sr += __shfl_xor(sr, 2, 64);
   const float smooth = sr + pn.snlastb[0] - pn.smooth0;
   const float decay = __expf(-0.5f * lbd);
+  // visit(d, X_d, (J^T X + net_out)_d) over this thread's dims
+  auto for_dims = [&](auto&& visit) {
+    if constexpr (X3) {
+      const int nxc = L.INP / 32 - 2;
+      for (int u = 0; u < nxc; ++u) {
+        float xv[8], gv[8], nv[8];
+        x3_get8(row, L.IN, 2 + u, q, xv);
+        x3_get8(row, L.GX, u, q, gv);
+        x3_get8(row, L.NO, u, q, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
+          if (d < nx) visit(d, xv[j], gv[j] + nv[j]);
+        }
+      }
+    } else {
+      const float* X = row + L.IN + PIS_IN_OFF;
+      for (int d = q; d < nx; d += 4) visit(d, X[d], row[L.GX + d] + row[L.NO + d]);
+    }
+  };
   // GMM responsibilities at y = decay * X  (g0 = -log p, grad g0(y) = sum_k w_k (y - mu_k) / var_k)
   float st[NSG];
 #pragma unroll
   for (int c = 0; c < NSG; ++c) st[c] = 0.f;
-  const float* X = row + L.IN + PIS_IN_OFF;
-  for (int d = q; d < nx; d += 4) {
-    const float y = decay * X[d];
+  for_dims([&](int d, float Xd, float) {
+    const float y = decay * Xd;
 #pragma unroll
     for (int c = 0; c < NSG; ++c)
       if (c < e.ncomp) {
         const float df = y - e.mean[c * nx + d];
         st[c] = fmaf(df * df, e.ivar[c * nx + d], st[c]);
       }
-  }
+  });
   float lp[NSG], mx = -3.0e38f;
 #pragma unroll
   for (int c = 0; c < NSG; ++c) {
@@ -202,16 +300,16 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
   }
   const float iws = 1.0f / ws;
   float A = 0.f, B = 0.f;
-  for (int d = q; d < nx; d += 4) {
-    const float y = decay * X[d];
+  for_dims([&](int d, float Xd, float jn) {
+    const float y = decay * Xd;
     float gg = 0.f;
 #pragma unroll
     for (int c = 0; c < NSG; ++c)
       if (c < e.ncomp) gg = fmaf(w[c] * iws, (y - e.mean[c * nx + d]) * e.ivar[c * nx + d], gg);
-    const float z = smooth * (row[L.GX + d] + row[L.NO + d]) + (1.0f - smooth) * decay * gg;
-    A = fmaf(X[d] - e.ou_mu, z, A);
+    const float z = smooth * jn + (1.0f - smooth) * decay * gg;
+    A = fmaf(Xd - e.ou_mu, z, A);
     B = fmaf(z, z, B);
-  }
+  });
   A += __shfl_xor(A, 1, 64);
   A += __shfl_xor(A, 2, 64);
   B += __shfl_xor(B, 1, 64);
@@ -222,19 +320,19 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
 }
 
 // Baseline f_b (state part) and nothing else: one 64-thread block per 16 points.
-template <int KIND>
+template <int KIND, bool X3>
 __global__ void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L, int n,
                                  float* __restrict__ fb) {
   const int i = blockIdx.x * 16 + (threadIdx.x >> 2), q = threadIdx.x & 3;
   const int ic = min(i, n - 1);
   const float* row = rows + (size_t)ic * L.stride;
   float A, B, sm;
-  pis_z_stats(e, pn, row, L, pn.T - row[L.SC + 0], q, A, B, sm);
+  pis_z_stats<X3>(e, pn, row, L, pn.T - row[L.SC + 0], q, A, B, sm);
   if (i < n && q == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, A, B);
 }
 
 // Per-path f, b_p and label contributions for one (point, 64-path block) -> partial slab.
-template <int KIND>
+template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                    int nbp, int K, int flags, const float* __restrict__ fbv,
                                                    const float* __restrict__ rows, PisRows L,
@@ -251,7 +349,7 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;
   const float s = row[L.SC + 0], ap = row[L.SC + 2], smt = row[L.SC + 3];
   float A, B, sm;
-  pis_z_stats(e, pn, row, L, pn.T - s, q, A, B, sm);
+  pis_z_stats<X3>(e, pn, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
   const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * smt) * e.asq);
   if (q == 0) {

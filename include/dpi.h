@@ -112,9 +112,10 @@ int dpi_net_destroy(dpi_net net);
 
 /* MFMA precision of the network evaluations.  DPI_GEMM_F32: v_mfma_f32_16x16x4_f32 everywhere.
  * DPI_GEMM_F16X3: fp16-split x = hi + 2^-11 lo, three v_mfma_f32_16x16x32_f16 per product
- * (~2.4e-7 relative error, same tolerance class as fp32) everywhere.  DPI_GEMM_AUTO (default):
- * fp16-split for the fused MLP of the path kernel (hidden width % 32 == 0), fp32 for the
- * PISGradNet GEMM pipeline.  The environment variable DPI_GEMM=f32|f16x3 sets the initial mode.
+ * (~2.4e-7 relative error, same tolerance class as fp32) everywhere: the fused MLP of the path
+ * kernel, and the PISGradNet pipeline with its activations stored split in HBM.
+ * DPI_GEMM_AUTO (default) = DPI_GEMM_F16X3.
+ * The environment variable DPI_GEMM=f32|f16x3 sets the initial mode.
  * Replaces no reference interface (the reference evaluates u in torch fp64/fp32). */
 #define DPI_GEMM_F32 0
 #define DPI_GEMM_F16X3 1

@@ -1,0 +1,28 @@
+"""Per-kernel VGPR/AGPR/spill/LDS of the built libdpi_hip.so (gfx950 code object metadata).
+usage: python tools/kernel_resources.py [name-substring ...]"""
+import re
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+lib = Path(__file__).resolve().parents[1] / "deeppicarditeration_amd" / "libdpi_hip.so"
+with tempfile.TemporaryDirectory() as d:
+    fb, co = f"{d}/fb.bin", f"{d}/gfx950.co"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", str(lib), fb], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True, text=True).stdout
+# kernel entries in amdhsa.kernels are YAML list items starting with "  - .agpr_count"
+for item in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
+    item = ".agpr_count:" + item
+    def g(k):
+        m = re.search(r"\." + k + r":\s+(\S+)", item)
+        return m.group(1) if m else "?"
+    name = g("name")
+    if len(sys.argv) > 1 and not any(s in name for s in sys.argv[1:]):
+        continue
+    dem = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+    print(f"vgpr {g('vgpr_count'):>4} agpr {g('agpr_count'):>4} spill {g('vgpr_spill_count'):>3} "
+          f"lds {g('group_segment_fixed_size'):>6}  {dem[:110]}")
