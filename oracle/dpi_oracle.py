@@ -13,6 +13,8 @@ Reference map (all paths relative to /root/reference):
                         picard/equations.py:118-124, :217-230 (sample_x / sample_x_ts)
   terminal estimator    picard/data.py:899-926 (estimate_terminal_with_gradients)
   integral estimator    picard/data.py:471-527 (estimate_integral_with_gradients), :350-366
+  TD estimators         picard/data.py:1209-1213 (ESTIMATE_DELTA_T > 0): :934-952
+                        (estimate_terminal_with_gradients_td), :529-575 (..._integral_..._td)
   get_f                 picard/data.py:1226-1325
   Cha                   picard/equations.py:266-338
   OUProcessEquation     picard/equations.py:489-714 + picard/utils.py:792-880 (GMM)
@@ -325,11 +327,22 @@ def _f_and_extras(eq, net, s, X, sdgd_idx=None, base_hdiag=None):
     return eq.ffi(s, X, u, uii), hd
 
 
+def td_horizon(eq, t, delta_t):
+    """t_next - t and whether the terminal value comes from u (t_next < T) for the TD estimators:
+    t_next = clip(t + delta_t, max=T) (picard/data.py:539, :940); delta_t = 0 is the plain
+    estimator (horizon T - t, terminal value g)."""
+    if delta_t > 0 and t + delta_t < eq.T:
+        return delta_t, True
+    return eq.T - t, False
+
+
 def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=1024,
-                return_parts=False):
+                return_parts=False, delta_t=0.0):
     """generate_with_gradients (picard/data.py:1208-1218) with K-step EM paths.
 
-    Returns y (n, 1+nx) = terminal + integral.  v > 0 enables SDGD indices (GBM)."""
+    Returns y (n, 1+nx) = terminal + integral.  v > 0 enables SDGD indices (GBM).
+    delta_t > 0 selects the TD estimators (data.py:1209-1213): horizon t_next = min(t + delta_t, T)
+    instead of T, terminal value u(t_next, X) where t_next < T (data.py:934-952, :529-575)."""
     tx = np.asarray(tx, np.float64)
     n = tx.shape[0]
     nx = eq.nx
@@ -341,6 +354,7 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
         ig = point_base + r
         t = tx[r, 0]
         x = tx[r:r + 1, 1:]
+        hmt, td_u = td_horizon(eq, t, delta_t)
         # per-point baselines
         g_x = eq.g(x)[0, 0]
         if eq.has_hessian_term:
@@ -353,16 +367,19 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
         for m0 in range(0, M, m_chunk):
             m = np.arange(m0, min(M, m0 + m_chunk))
             S_T, S_s, U, idx = path_noise(eq, ig, m, K, seed, epoch, v)
-            # terminal (data.py:899-926)
-            hT = (T - t) / K
+            # terminal (data.py:899-926; TD :934-952)
+            hT = hmt / K
             W_T = math.sqrt(hT) * S_T
             XT = x + a * W_T
-            Y = W_T / (T - t) / a
-            c = (eq.g(XT) - g_x)
+            Y = W_T / hmt / a
+            if td_u:
+                c = net.value_grad(np.concatenate([np.full((len(m), 1), t + delta_t), XT], -1))[0] - g_x
+            else:
+                c = (eq.g(XT) - g_x)
             term[r, 0] += c.sum()
             term[r, 1:] += (c * Y).sum(0)
-            # integral (data.py:471-527, 350-366)
-            s = (U * (T - t) + t)[:, None]
+            # integral (data.py:471-527, 350-366; TD :529-575)
+            s = (U * hmt + t)[:, None]
             W_s = np.sqrt((s - t) / K) * S_s
             Xs = x + a * W_s
             Ys = W_s / (s - t) / a
@@ -374,8 +391,8 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
             else:
                 f, _ = _f_and_extras(eq, net, s, Xs)
                 fb = np.full((len(m), 1), fb_plain)
-            cI = (T - t) * (f - fb)
-            integ[r, 0] += cI.sum() + (fb * (T - t)).sum()
+            cI = hmt * (f - fb)
+            integ[r, 0] += cI.sum() + (fb * hmt).sum()
             integ[r, 1:] += (cI * Ys).sum(0)
         term[r] /= M
         integ[r] /= M
@@ -455,10 +472,10 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
     return y
 
 
-def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf):
+def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf, delta_t=0.0):
     """picard/data.py:211-223: (tx, clip(y))."""
     tx = sample_points(eq, n, seed, epoch, point_base)
-    y = labels_grad(eq, net, tx, M, K, seed, epoch, point_base, v)
+    y = labels_grad(eq, net, tx, M, K, seed, epoch, point_base, v, delta_t=delta_t)
     return tx, np.clip(y, -sample_bound, sample_bound)
 
 
@@ -473,24 +490,28 @@ def rel_l2_parts(a, b):
 
 
 # ----------------------------------------------------------------------------- moments (sharding)
-def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0):
+def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0, delta_t=0.0):
     """Per-path contribution rows c (len(m), 1+nx) whose mean (+ g(x) in column 0) is the label
-    (picard/data.py:923-925, :523-526), for one point and MC indices m."""
+    (picard/data.py:923-925, :523-526; TD :947-951, :570-574), for one point and MC indices m."""
     t = float(tx_row[0])
     x = np.asarray(tx_row[1:], np.float64)[None]
-    T, a = eq.T, eq.alpha_sqrt
+    a = eq.alpha_sqrt
+    hmt, td_u = td_horizon(eq, t, delta_t)
     g_x = eq.g(x)[0, 0]
     fb = _f_and_extras(eq, net, np.array([[t]]), x)[0][0, 0]
     S_T, S_s, U, _ = path_noise(eq, ig, np.asarray(m), K, seed, epoch)
-    W_T = math.sqrt((T - t) / K) * S_T
-    Y = W_T / (T - t) / a
-    cT = eq.g(x + a * W_T) - g_x
-    s = (U * (T - t) + t)[:, None]
+    W_T = math.sqrt(hmt / K) * S_T
+    Y = W_T / hmt / a
+    if td_u:
+        cT = net.value_grad(np.concatenate([np.full((len(m), 1), t + delta_t), x + a * W_T], -1))[0] - g_x
+    else:
+        cT = eq.g(x + a * W_T) - g_x
+    s = (U * hmt + t)[:, None]
     W_s = np.sqrt((s - t) / K) * S_s
     f, _ = _f_and_extras(eq, net, s, x + a * W_s)
-    cI = (T - t) * (f - fb)
+    cI = hmt * (f - fb)
     Ys = W_s / (s - t) / a
-    c = np.concatenate([cT + cI + fb * (T - t), cT * Y + cI * Ys], -1)
+    c = np.concatenate([cT + cI + fb * hmt, cT * Y + cI * Ys], -1)
     return c, g_x
 
 

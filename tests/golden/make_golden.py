@@ -216,7 +216,7 @@ def state_dict_np(module):
 
 
 def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, point_base=0, v=0,
-             init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False):
+             init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False, delta_t=0.0):
     torch.set_default_dtype(torch.float64)
     eq = make_equation(eq_name, eq_kw, workdir)
     torch.manual_seed(init_seed)
@@ -237,7 +237,7 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
     gen = data.OnlineDataGenerator(
         eq, net, 1, 1, device="cpu", t_always_uniform=True, n_estimate_terminal=M,
         n_estimate_integral=M, hessian_approximation=hess, sample_bound=None,
-        estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=0.0)
+        estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=delta_t)
     if hessians:
         items = noise_items_hess(eq.nx, n, M, K, seed, epoch, point_base)
         with NoiseQueue(items):
@@ -249,6 +249,7 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
     out = {
         "case": name, "eq": eq_name, "net": "zero" if zero else net_kind, "n": n, "M": M, "K": K,
         "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v, "hessians": hessians,
+        "delta_t": delta_t,
         "tx": tx.numpy(), "y": y.detach().numpy(),
     }
     for k, val in eq_kw.items():
@@ -304,6 +305,18 @@ def main(only=None):
              epoch=2, point_base=5, workdir=wd, hessians=True)
     run_case("gbm_hess_zero_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [8]}, 2, 64, 2, 9,
              workdir=wd, zero=True, hessians=True)
+    # TD estimators (DATA.ESTIMATE_DELTA_T > 0, data.py:1209-1213): points on both sides of
+    # t + delta_t = T (n = 8 points, t ~ U(0.01, 0.99))
+    run_case("td_cha_mlp16_K2", "Cha", cha, "mlp", {"neurons": [16, 16]}, 8, 64, 2, 21, workdir=wd, delta_t=0.3)
+    run_case("td_cha_mlp64x3_K5", "Cha", cha, "mlp", {"neurons": [64] * 3}, 6, 64, 5, 22, epoch=2, workdir=wd,
+             delta_t=0.45)
+    run_case("td_cha_zero_K1", "Cha", cha, "mlp", {"neurons": [8]}, 6, 64, 1, 23, workdir=wd, zero=True, delta_t=0.2)
+    run_case("td_ou_mlp32_K3", "OUProcessEquation", ou, "mlp", {"neurons": [32, 32]}, 6, 64, 3, 24, workdir=wd,
+             delta_t=0.35)
+    run_case("td_gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 6, 64, 2, 25,
+             v=100, workdir=wd, delta_t=0.4)
+    run_case("td_ou_pis32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 6, 64, 2, 26, workdir=wd,
+             delta_t=0.55)
     shutil.rmtree(wd)
 
 
