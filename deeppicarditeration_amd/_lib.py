@@ -32,6 +32,7 @@ SIGNATURES = {
                                       P(c_double), P(c_double), P(c_double), P(c_void_p)]),
     "dpi_problem_create_gbm": (c_int, [c_int, c_double, c_double, c_int, P(c_double), P(c_double), P(c_void_p)]),
     "dpi_problem_set_hessian_approximation": (c_int, [c_void_p, c_int]),
+    "dpi_problem_set_estimate_delta_t": (c_int, [c_void_p, c_double]),
     "dpi_problem_destroy": (c_int, [c_void_p]),
     "dpi_net_create_zero": (c_int, [P(c_void_p)]),
     "dpi_net_create_mlp": (c_int, [c_int, c_int, P(c_int), c_int, P(c_float), c_size_t, P(c_void_p)]),

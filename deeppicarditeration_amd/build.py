@@ -1,7 +1,8 @@
 """Build libdpi_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
 
-Four translation units (the C-ABI / PIS / reduce TU and one k_paths family per equation) compile
-in parallel to objects, then link into one shared library."""
+Seven translation units (the C-ABI / PIS / reduce TU, one k_paths family per equation and one
+TD-estimator k_paths family per equation) compile in parallel to objects, then link into one
+shared library."""
 import os
 import subprocess
 import sys
@@ -11,7 +12,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 REPO = ROOT.parent
 CSRC = ROOT / "csrc"
-UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_gbm.hip"]
+UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_gbm.hip", "dpi_paths_td_cha.hip",
+         "dpi_paths_td_ou.hip", "dpi_paths_td_gbm.hip"]
 OBJ = ROOT / "build"
 OUT = ROOT / "libdpi_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

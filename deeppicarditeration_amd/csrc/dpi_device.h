@@ -735,6 +735,62 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
   s2_out = s2;
 }
 
+// u(tau, x + cmul S) for this wave's 16 paths with every weight LDS-resident (GBM layout):
+// the forward half of mlp_hdiag.  The TD terminal value (data.py:941-942).
+template <int H, int L>
+__device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh, int nxt) {
+  constexpr int HT = H / 16;
+  constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  float act[L][HT][4];
+#pragma unroll
+  for (int T = 0; T < HT; ++T) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    for (int t = 0; t < nxt; ++t) {
+      const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+      const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+      acc = mfma4(a.x, bc[0], acc);
+      acc = mfma4(a.y, bc[SS], acc);
+      acc = mfma4(a.z, bc[2 * SS], acc);
+      acc = mfma4(a.w, bc[3 * SS], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* wrow = sh.Wh[l - 1] + (16 * T + jj) * WHS + 4 * qq;
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+        acc = mfma4(a.x, act[l - 1][t][0], acc);
+        acc = mfma4(a.y, act[l - 1][t][1], acc);
+        acc = mfma4(a.z, act[l - 1][t][2], acc);
+        acc = mfma4(a.w, act[l - 1][t][3], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+    }
+  }
+  float up = 0.f;
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) up = fmaf(sh.vec[2 * H + 16 * T + 4 * qq + r], act[L - 1][T][r], up);
+  return qsum(up) + net.bout;
+}
+
 // ------------------------------------------------------------------------------ kernels
 // Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
 template <int KIND>
@@ -986,6 +1042,9 @@ struct PathArgs {
   int split;  // fused MLP on the fp16-split MFMA
   float* hpart;            // Hessian labels: block sums [n][nbp][nx*nx]
   uint32_t c3h1, c3h2;     // Hessian labels: Malliavin normal streams (tags HTERM, HINT)
+  // DATA.ESTIMATE_DELTA_T (data.py:1209-1213): > 0 selects the TD estimators (k_paths<.., TD>),
+  // horizon t_next = min(t + td_dt, T), terminal value u(t_next, X) where t_next < T
+  float td_dt;
 };
 
 // ------------------------------------------------------------------------------ Hessian labels
@@ -1165,9 +1224,14 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
 }
 
 // One workgroup = (point i, 64 consecutive MC indices).  See the file header.
-template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false>
-__global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+// TD: the TD estimators (ESTIMATE_DELTA_T > 0, data.py:1209-1213, :934-952, :529-575): every
+// T - t below becomes the horizon t_next - t, and where t_next = t + dt < T (workgroup-uniform:
+// one point per workgroup) the terminal value is u(t_next, X_{t_next}), evaluated by the same MLP
+// tile on the terminal noise before the integral rollout takes the noise tile.
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false>
+__global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
+  static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
@@ -1181,7 +1245,13 @@ __global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev
   const bool TERM = a.flags & DPI_TERMINAL, INTG = a.flags & DPI_INTEGRAL;
   const float* txr = a.tx + (size_t)i * F;
   const float t = txr[0];
-  const float tmt = e.T - t;
+  // horizon: T - t, or for TD t_next - t = dt where t_next = t + dt < T (data.py:539, :940)
+  bool td_u = false;
+  float tmt = e.T - t;
+  if constexpr (TD) {
+    td_u = t + a.td_dt < e.T;
+    if (td_u) tmt = a.td_dt;
+  }
   const float g_x = a.gx[i], f_b = a.fb[i];
   const float Kf = (float)a.K;
 
@@ -1401,7 +1471,9 @@ __global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev
   // opposite orders overlaps one's MFMA phase with the other's VALU phase.  The results do not
   // depend on the order (same counters, same per-lane arithmetic).
   bool tlast = false;
-  if constexpr (SPLIT) {
+  if constexpr (TD) {
+    tlast = false;  // the terminal MLP needs the noise tile before the integral rollout
+  } else if constexpr (SPLIT) {
     tlast = true;  // measured faster, and the terminal sums are not live across the MLP (no spills)
   } else if constexpr (!GBM) {
     if (a.order == 1) tlast = (__builtin_amdgcn_s_getreg((3 << 11) | (16 << 6) | 4) & 1) != 0;  // HW_ID.TG_ID
@@ -1409,8 +1481,57 @@ __global__ __launch_bounds__(256, KIND == DPI_EQ_GBM ? 1 : 2) void k_paths(EqDev
     else if (a.order == 3) tlast = ((blockIdx.x >> 8) & 1) != 0;
     else if (a.order == 4) tlast = true;
   }
+  // TD terminal value u(t_next, x + cT S_T) (data.py:941-942), per lane = path
+  [[maybe_unused]] auto terminal_value_td = [&]() -> float {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int j = wv + 4 * c;
+      if (j < nb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          sh.S[d * SS + lane] = d < nx ? ST[c][q] : 0.f;
+        }
+    }
+    if (wv == 0) {
+      sh.tau[lane] = t + a.td_dt;
+      sh.cmul[lane] = cT;
+    }
+    __syncthreads();
+    float u = 0.f;
+    if constexpr (!ZERO) {
+      if constexpr (GBM) {
+        u = mlp_value_res<H, L>(net, sh, nxp / 16);
+      } else {
+        float gs, gA, gB;
+        if constexpr (SPLIT)
+          mlp_tile_split<KIND, H, L>(e, net, sh, u, gs, gA, gB);
+        else
+          mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
+      }
+    }
+    const int pp = 16 * wv + (lane & 15);
+    if ((lane >> 4) == 0) sh.bsh[pp] = u;
+    __syncthreads();
+    const float uT = sh.bsh[lane];
+    if (wv == 0) {
+      sh.tau[lane] = s;
+      sh.cmul[lane] = cI;
+    }
+    // the integral rollout's writes into S are published by terminal_finish's barrier
+    return uT;
+  };
   float ap;
-  if (!tlast) {
+  if constexpr (TD) {
+    terminal_rollout();
+    float uT = 0.f;
+    if (td_u && TERM) uT = terminal_value_td();
+    integral_rollout();
+    ap = terminal_finish();
+    if (td_u) ap = TERM ? uT - g_x : 0.f;  // (u(t_next, X) - g(x)) (data.py:942, :947)
+    integrand();
+    __syncthreads();
+  } else if (!tlast) {
     terminal_rollout();
     integral_rollout();
     ap = terminal_finish();

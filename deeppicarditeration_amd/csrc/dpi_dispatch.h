@@ -8,6 +8,7 @@ using namespace dpi;
 
 struct dpi_problem_s {
   EqDev e;
+  float td_dt = 0.f;  // DATA.ESTIMATE_DELTA_T (dpi_problem_set_estimate_delta_t)
   float alpha_init_sqrt;
   std::vector<void*> dev;
 };
@@ -29,11 +30,27 @@ struct Launch {
   int nblocks;
   hipStream_t st;
   bool hess = false;  // k_paths in Hessian-label mode (GBM only)
+  bool td = false;    // k_paths with the TD estimators (problem td_dt > 0)
 };
 
-template <int KIND, int H, int L, bool Z>
+// TDV: the TD-estimator k_paths variants, compiled in translation units of their own
+// (dpi_paths_td_*.hip): sharing a unit with the plain kernels perturbs the register allocation
+// of the plain fused-MLP kernel (6 spills at 256 VGPRs instead of none at 252).
+template <int KIND, int H, int L, bool Z, bool TDV>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
-  if (q.baseline)
+  if constexpr (TDV) {
+    if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+      if (q.a->split)
+        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+                           net->d, *q.a);
+      else
+        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+                           net->d, *q.a);
+    } else {
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+                         net->d, *q.a);
+    }
+  } else if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                        q.bx, q.hb);
   else if (q.hess) {
@@ -52,22 +69,24 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
     hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
 }
 
-template <int KIND>
+template <int KIND, bool TDV = false>
 bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if (net->d.kind == 0) {
-    do_launch<KIND, 16, 1, true>(p, net, q);
+    do_launch<KIND, 16, 1, true, TDV>(p, net, q);
     return true;
   }
   const int H = net->d.H, L = net->d.L;
-  if (q.baseline) {  // the baseline kernel is shape-generic
-    if (KIND == DPI_EQ_GBM && H > 64) return false;
-    do_launch<KIND, 16, 1, false>(p, net, q);
-    return true;
+  if constexpr (!TDV) {
+    if (q.baseline) {  // the baseline kernel is shape-generic
+      if (KIND == DPI_EQ_GBM && H > 64) return false;
+      do_launch<KIND, 16, 1, false, false>(p, net, q);
+      return true;
+    }
   }
   if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
 #define DPI_SHAPE(HH, LL)                      \
   if (H == HH && L == LL) {                    \
-    do_launch<KIND, HH, LL, false>(p, net, q); \
+    do_launch<KIND, HH, LL, false, TDV>(p, net, q); \
     return true;                               \
   }
     DPI_SHAPE(64, 3)
@@ -96,3 +115,6 @@ bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q)
 bool dispatch_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

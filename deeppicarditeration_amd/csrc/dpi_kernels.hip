@@ -272,6 +272,12 @@ int dpi_problem_set_hessian_approximation(dpi_problem p, int sdgd_v) {
   return 0;
 }
 
+int dpi_problem_set_estimate_delta_t(dpi_problem p, double delta_t) {
+  if (!p || !(delta_t >= 0.0) || !(delta_t < 1e30)) return fail(DPI_ERR_ARG, "estimate_delta_t: 0 <= dt < inf");
+  p->td_dt = (float)delta_t;
+  return 0;
+}
+
 int dpi_problem_destroy(dpi_problem p) {
   if (!p) return 0;
   for (void* d : p->dev) (void)hipFree(d);
@@ -850,13 +856,14 @@ extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t e
 }
 
 static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  const bool td = q.td && !q.baseline && !q.hess;
   switch (p->e.kind) {
     case DPI_EQ_CHA:
-      return dispatch_cha(p, net, q);
+      return td ? dispatch_td_cha(p, net, q) : dispatch_cha(p, net, q);
     case DPI_EQ_OU:
-      return dispatch_ou(p, net, q);
+      return td ? dispatch_td_ou(p, net, q) : dispatch_ou(p, net, q);
     case DPI_EQ_GBM:
-      return dispatch_gbm(p, net, q);
+      return td ? dispatch_td_gbm(p, net, q) : dispatch_gbm(p, net, q);
     default:
       return false;
   }
@@ -975,6 +982,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   char* b = (char*)ws;
   float* partial = (float*)(b + w.partial);
   PathArgs a;
+  std::memset(&a, 0, sizeof(a));
   a.tx = tx;
   a.gx = (const float*)(b + w.gx);
   a.fb = (const float*)(b + w.fb);
@@ -995,11 +1003,15 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.point_base = point_base;
   a.order = path_order();
   a.split = mlp_split() ? 1 : 0;
+  a.td_dt = p->td_dt;
   hipStream_t st = (hipStream_t)stream;
   if (net->d.kind == 2) {
+    if (p->td_dt > 0.f)
+      return fail(DPI_ERR_UNSUPPORTED, "label_moments: TD estimators (estimate_delta_t > 0) with PISGradNet");
     if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st))) return rc;
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
+    q.td = p->td_dt > 0.f;
     if (!dispatch_any(p, net, q))
       return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
   }

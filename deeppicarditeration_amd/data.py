@@ -15,6 +15,9 @@ Differences from the reference, by design:
   distribution, and pathwise when the reference is fed xi_eff = sum_k xi_k / sqrt(K);
 - tensors are fp32 on the GPU (the YAMLs say DATA.FLOAT: double; parity is measured against
   the fp64 reference, tests/test_gpu_parity.py).
+
+`estimate_delta_t > 0` selects the reference's TD estimators (data.py:1209-1213) on the device
+(MLP and zero networks).
 """
 from typing import Union
 
@@ -64,8 +67,9 @@ class OnlineDataGenerator:
             raise AssertionError("Currently only nu=1 is supported")
         if not t_always_uniform:
             raise NotImplementedError("t_always_uniform=False (product-of-uniforms t sampler) is not built yet")
-        if estimate_delta_t and estimate_delta_t > 0:
-            raise NotImplementedError("TD estimators (ESTIMATE_DELTA_T > 0) are out of scope for this build")
+        self.estimate_delta_t = float(estimate_delta_t or 0.0)
+        if self.estimate_delta_t < 0:
+            raise ValueError(f"estimate_delta_t must be >= 0 (got {estimate_delta_t})")
         method, sdgd_v = _hessian_approximation(hessian_approximation)
         if method is not None:  # data.py:115-123
             if method not in equation.supported_approximate_methods:
@@ -101,11 +105,19 @@ class OnlineDataGenerator:
         solution.eval()
         self.net = DeviceNet.from_module(solution, 1 + equation.nx)
         self.problem = equation.dpi_problem()
-        if equation.has_hessian_term:
-            _lib.check(self.lib.dpi_problem_set_hessian_approximation(self.problem, sdgd_v),
-                       "dpi_problem_set_hessian_approximation")
         self.sdgd_v = sdgd_v
+        self._configure_problem()
         self._ws = None
+
+    def _configure_problem(self):
+        """The device problem handle belongs to the equation and may be shared by several
+        generators: (re)apply this generator's estimator settings before each label call."""
+        if self.equation.has_hessian_term:
+            _lib.check(self.lib.dpi_problem_set_hessian_approximation(self.problem, self.sdgd_v),
+                       "dpi_problem_set_hessian_approximation")
+        # TD estimators (data.py:1209-1213); 0 = the plain estimators
+        _lib.check(self.lib.dpi_problem_set_estimate_delta_t(self.problem, self.estimate_delta_t),
+                   "dpi_problem_set_estimate_delta_t")
 
     # ------------------------------------------------------------------ buffers
     def _workspace(self, n, M, hessians=False):
@@ -178,6 +190,7 @@ class OnlineDataGenerator:
         """Sum / sum-of-squares of per-path contributions over m in [m_begin, m_end): (n, 2, 1+nx)."""
         n = tx.shape[0]
         mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        self._configure_problem()
         _lib.check(self.lib.dpi_label_moments(self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed,
                                               self.epoch, point_base, m_begin, m_end, flags, _ptr(mom), _ptr(ws),
                                               ws.numel(), _stream(self.device)), "dpi_label_moments")
@@ -196,6 +209,7 @@ class OnlineDataGenerator:
         n, nx = tx.shape[0], self.equation.nx
         mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self.device)
         hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self.device)
+        self._configure_problem()
         _lib.check(self.lib.dpi_label_moments_hessians(
             self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, point_base, m_begin, m_end,
             _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_label_moments_hessians")
@@ -236,6 +250,7 @@ class OnlineDataGenerator:
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self.device)
+        self._configure_problem()
         _lib.check(self.lib.dpi_generate_with_gradients_and_hessians(
             self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, bound, _ptr(y),
             _ptr(self._ws), self._ws.numel(), _stream(self.device)), "dpi_generate_with_gradients_and_hessians")
@@ -257,6 +272,7 @@ class OnlineDataGenerator:
             y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
             self.last_moments = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
             b = self.sample_bound if bound is None else bound
+            self._configure_problem()
             _lib.check(self.lib.dpi_generate_with_gradients(
                 self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, flags, b, _ptr(y),
                 _ptr(self.last_moments), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_generate_with_gradients")

@@ -13,6 +13,7 @@
  *   dpi_problem_create_ou    picard/equations.py:489-714  OUProcessEquation(...) + utils.py:792-914 GMM
  *   dpi_problem_create_gbm   picard/equations.py:388-486  GBMEquationComplexExact(nx, alpha, T)
  *   dpi_problem_set_hessian_approximation  picard/data.py:115-123, :497-502  HESSIAN_APPROXIMATION (SDGD v)
+ *   dpi_problem_set_estimate_delta_t  picard/data.py:1209-1213, :934-952, :529-575  ESTIMATE_DELTA_T (TD estimators)
  *   dpi_net_create_zero      picard/solution.py:330-337   ZeroSolution (iteration 1)
  *   dpi_net_create_mlp       picard/solution.py:123-135   construct_mlp (state-dict order)
  *   dpi_net_create_pisgrad   picard/solution.py:138-289   PISGradNet (state-dict order)
@@ -93,6 +94,13 @@ int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const do
  * Hessian diagonal (picard/data.py:1262-1272); 1 <= sdgd_v <= 255 draws v indices in [0, nx)
  * with replacement per path (SDGD, data.py:497-502, 1273-1303). */
 int dpi_problem_set_hessian_approximation(dpi_problem p, int sdgd_v);
+/* DATA.ESTIMATE_DELTA_T: delta_t > 0 selects the TD estimators of generate_with_gradients
+ * (estimate_terminal_with_gradients_td, estimate_integral_with_gradients_td): per point the
+ * horizon is t_next = min(t + delta_t, T) instead of T, s ~ U(t, t_next], and the terminal value
+ * is u(t_next, X_{t_next}) (the network) where t_next < T, g(X_T) otherwise.  0 (default) = the
+ * plain estimators.  MLP and zero networks (PISGradNet: DPI_ERR_UNSUPPORTED); the Hessian-label
+ * entry points ignore it, as the reference's generate_with_gradients_and_hessians does. */
+int dpi_problem_set_estimate_delta_t(dpi_problem p, double delta_t);
 int dpi_problem_destroy(dpi_problem p);
 
 /* --- networks u(t, x): weights uploaded once per Picard iteration into a library handle --- */

@@ -3,7 +3,7 @@ import numpy as np
 import torch
 
 import deeppicarditeration_amd as dpi
-from golden_util import state_dict
+from golden_util import delta_t, state_dict
 
 
 def product_equation(f):
@@ -42,7 +42,8 @@ def generator(f, eq, module, M=None, K=None):
     hess = {"method": "SDGD", "kwargs": {"v": v}} if v > 0 else None
     return dpi.OnlineDataGenerator(eq, module, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
                                    n_estimate_integral=M, n_euler_steps=int(f["K"]) if K is None else K,
-                                   seed=int(f["seed"]), epoch=int(f["epoch"]), hessian_approximation=hess)
+                                   seed=int(f["seed"]), epoch=int(f["epoch"]), hessian_approximation=hess,
+                                   estimate_delta_t=delta_t(f))
 
 
 def rel_l2_parts(a, b):

@@ -22,11 +22,12 @@ def _need_gpu():
     L.load()  # fail loudly if the HIP library is missing
 
 
-from golden_util import CASES, load, oracle_equation, oracle_net  # noqa: E402
+from golden_util import CASES, delta_t, load, oracle_equation, oracle_net  # noqa: E402
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
-SUPPORTED = list(CASES)
+# TD estimators with PISGradNet are not built (dpi_problem_set_estimate_delta_t): they raise
+SUPPORTED = [c for c in CASES if not (c.startswith("td_") and "pis" in c)]
 
 
 @pytest.mark.parametrize("case", SUPPORTED)
@@ -74,6 +75,53 @@ def test_terminal_and_integral_estimators(case):
     assert pI["value"] < TOL and pI["grad"] < TOL, pI
 
 
+@pytest.mark.parametrize("case", ["td_cha_mlp16_K2", "td_ou_mlp32_K3", "td_gbm_mlp16_sdgd_K2", "td_cha_zero_K1"])
+def test_td_terminal_and_integral_estimators(case):
+    """TD estimators (ESTIMATE_DELTA_T > 0): estimate_terminal_with_gradients_td (data.py:934-952)
+    and estimate_integral_with_gradients_td (:529-575) separately vs the oracle."""
+    f = load(case)
+    eq = product_equation(f)
+    oeq = oracle_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    pb = int(f["point_base"])
+    yT = gen.estimate_terminal_with_gradients(tx, point_base=pb).cpu().numpy()
+    yI = gen.estimate_integral_with_gradients(tx, point_base=pb).cpu().numpy()
+    _, rT, rI = O.labels_grad(oeq, oracle_net(f, oeq), f["tx"], int(f["M"]), int(f["K"]), int(f["seed"]),
+                              int(f["epoch"]), pb, v=int(f["v"]), return_parts=True, delta_t=delta_t(f))
+    pT, pI = rel_l2_parts(yT, rT), rel_l2_parts(yI, rI)
+    assert pT["value"] < TOL and pT["grad"] < TOL, pT
+    assert pI["value"] < TOL and pI["grad"] < TOL, pI
+
+
+def test_td_pisgradnet_fails_loudly():
+    from deeppicarditeration_amd._lib import DPIError
+    f = load("td_ou_pis32_K2")
+    eq = product_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    with pytest.raises(DPIError):
+        gen.generate_with_gradients(torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0"))
+
+
+def test_td_generator_does_not_leak_into_shared_problem():
+    """Two generators on one equation object (one device problem handle), TD and plain: each
+    call applies its own estimator settings."""
+    f = load("cha_mlp16_K4")
+    eq = product_equation(f)
+    net = product_module(f, eq)
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    plain = generator(f, eq, net)
+    y0 = plain.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu()
+    import deeppicarditeration_amd as dpi
+    td = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                 n_estimate_integral=64, n_euler_steps=int(f["K"]), seed=int(f["seed"]),
+                                 epoch=int(f["epoch"]), estimate_delta_t=0.1)
+    y_td = td.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu()
+    y1 = plain.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu()
+    assert torch.equal(y0, y1)
+    assert not torch.equal(y0, y_td)
+
+
 def _random_mlp(eq, widths, seed):
     import deeppicarditeration_amd as dpi
     torch.manual_seed(seed)
@@ -108,6 +156,25 @@ def test_burgers_full_network_K50_vs_oracle(mlp_precision):
     ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 512, 50, 1, 0, 0)
     parts = rel_l2_parts(y.cpu().numpy(), ref)
     print("mlp precision", mlp_precision, parts)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_td_burgers_full_network_K50_vs_oracle(mlp_precision):
+    """TD estimators with the config-2 network (4x128 ELU), K = 50: the split / fp32 fused MLP
+    evaluates u(t_next, X) on the terminal noise, then u, grad u on the integral noise."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    net = _random_mlp(eq, [128] * 4, 0)
+    M, K, n, dt = 128, 50, 8, 0.25
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1, estimate_delta_t=dt)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    t = tx[:, 0].cpu().numpy()
+    assert (t + dt < 1).any() and (t + dt >= 1).any()  # t = 0.81, 0.06, 0.18, 0.87, ...
+    y = gen.generate_with_gradients(tx, point_base=0).cpu().numpy()
+    ref = O.labels_grad(O.Cha(100, 1.0, 5.0, 1.0), _oracle_mlp(net), tx.cpu().double().numpy(), M, K, 1, 1, 0,
+                        delta_t=dt)
+    parts = rel_l2_parts(y, ref)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 

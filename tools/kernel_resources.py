@@ -11,9 +11,19 @@ lib = Path(__file__).resolve().parents[1] / "deeppicarditeration_amd" / "libdpi_
 with tempfile.TemporaryDirectory() as d:
     fb, co = f"{d}/fb.bin", f"{d}/gfx950.co"
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", str(lib), fb], check=True)
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True, text=True).stdout
+    # a multi-TU library carries one offload bundle per translation unit: unbundle each
+    data = Path(fb).read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [i for i in range(len(data)) if data.startswith(magic, i)]
+    notes = ""
+    for k, st in enumerate(starts):
+        part = f"{d}/p{k}.bin"
+        Path(part).write_bytes(data[st:starts[k + 1] if k + 1 < len(starts) else len(data)])
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}.{k}"], capture_output=True)
+        if r.returncode == 0:
+            notes += subprocess.run([f"{LLVM}/llvm-readelf", "--notes", f"{co}.{k}"], check=True, capture_output=True,
+                                    text=True).stdout
 # kernel entries in amdhsa.kernels are YAML list items starting with "  - .agpr_count"
 for item in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
     item = ".agpr_count:" + item
