@@ -748,7 +748,7 @@ static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, const flo
 
 // The PISGradNet chain of pis_chain in split storage (every width padded to 32; the x part of IN
 // starts at its chunk 2 = word 64).
-static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t st) {
+static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t st, bool vjp = true) {
   PisRows L = pis_rows_layout(pd, true);
   auto r64 = [](int x) { return (x + 63) & ~63; };
   const int ld = L.stride, C = PIS_CH, NXK = (pd.nx + 31) & ~31, NOP = r64(pd.nx);
@@ -768,6 +768,8 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
     Kp = r64(pd.h[l]);
   }
   gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
+  L.H0 = hs;
+  if (!vjp) return L;
   // VJP: the x part of IN starts at its chunk 2 (word 64)
   int dcur = L.D0, dnext = L.D1;
   gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld, nullptr,
@@ -784,7 +786,7 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
 
 // PISGradNet forward + VJP over R rows (solution.py:256-289); returns the row layout with H0 pointing
 // at the last smooth_net activation.
-static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st) {
+static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st, bool vjp = true) {
   PisRows L = pis_rows_layout(pd, false);
   const int ld = L.stride, C = PIS_CH, nx = pd.nx;
   // t_encoder -> IN[:, 0:64]
@@ -806,6 +808,8 @@ static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st
     in = pd.h[l];
   }
   gemm(EPI_BIAS, R, nx, in, a, ld, pd.nn[pd.L], in, rows + L.NO, ld, pd.nnb[pd.L], nullptr, 0, st);
+  L.H0 = hs;
+  if (!vjp) return L;
   // VJP with cotangent X on net_out: D_{L-1} = (X nn_L) * elu'(A_{L-1}), ..., GX = D_0 nn_0[:, 64:]
   int dcur = L.D0, dnext = L.D1;
   gemm(EPI_DELU, R, pd.h[pd.L - 1], nx, rows + L.IN + PIS_IN_OFF, ld, pd.nnT[pd.L], nx, rows + dcur, ld, nullptr,
@@ -923,21 +927,40 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
   const bool x3 = pis_x3(net->pis);
   const PisRows L = pis_rows_layout(net->pis, x3);
   const int G = n * a.nbp, GC = std::max(1, w.rows_cap / P);
+  const float dt = a.td_dt;
+  // TD estimators: a terminal stage (rollout to t_next, forward chain, a_p = u(t_next, X) - g(x))
+  // before the integral stage; the plain estimators run both paths in one rollout.
+  auto chunk = [&](auto x3c, int g0, int g) {
+    constexpr bool X3 = decltype(x3c)::value;
+    auto chain = [&](bool vjp) {
+      return X3 ? pis_chain_x3(net->pis, rows, g * P, st, vjp) : pis_chain(net->pis, rows, g * P, st, vjp);
+    };
+    auto rollout = [&](int stage) {
+      hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp,
+                         a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L, stage,
+                         dt);
+    };
+    if (dt > 0.f) {
+      rollout(PIS_TD_TERM);
+      if (a.flags & DPI_TERMINAL) {
+        const PisRows Lt = chain(false);
+        hipLaunchKernelGGL((k_pis_tvalue<DPI_EQ_OU, X3>), dim3(g), dim3(256), 0, st, p->e, net->pis, tx, g0, a.nbp,
+                           a.gx, rows, Lt, g * P, dt);
+      }
+      rollout(PIS_TD_INT);
+    } else {
+      rollout(PIS_BOTH);
+    }
+    const PisRows Lc = chain(true);
+    hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
+                       a.flags, a.fb, rows, Lc, a.partial, dt);
+  };
   for (int g0 = 0; g0 < G; g0 += GC) {
     const int g = std::min(GC, G - g0);
-    if (x3) {
-      hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, true>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp,
-                         a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L);
-      const PisRows Lc = pis_chain_x3(net->pis, rows, g * P, st);
-      hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, true>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
-                         a.flags, a.fb, rows, Lc, a.partial);
-    } else {
-      hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, false>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp,
-                         a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L);
-      const PisRows Lc = pis_chain(net->pis, rows, g * P, st);
-      hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, false>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
-                         a.flags, a.fb, rows, Lc, a.partial);
-    }
+    if (x3)
+      chunk(std::true_type{}, g0, g);
+    else
+      chunk(std::false_type{}, g0, g);
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -1006,8 +1029,6 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.td_dt = p->td_dt;
   hipStream_t st = (hipStream_t)stream;
   if (net->d.kind == 2) {
-    if (p->td_dt > 0.f)
-      return fail(DPI_ERR_UNSUPPORTED, "label_moments: TD estimators (estimate_delta_t > 0) with PISGradNet");
     if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st))) return rc;
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};

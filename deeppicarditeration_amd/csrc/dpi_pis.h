@@ -72,12 +72,23 @@ struct PisRows {
 
 // Per-path rollout for the PIS pipeline (phase 1 of k_paths, outputs to global rows).
 // Block = (point, 64-path block) number g0 + blockIdx.x; row r = blockIdx.x * 64 + lane.
+// TD estimators (td_dt > 0, data.py:934-952, :529-575): horizon t_next - t instead of T - t, run
+// in two stages — stage PIS_TD_TERM rolls out the terminal path and writes the network input
+// rows at (t_next, X_{t_next}) (the forward chain and k_pis_tvalue then replace a_p by
+// u(t_next, X) - g(x) where t_next < T), stage PIS_TD_INT the integral path (ST and a_p kept).
+enum PisStage : int { PIS_BOTH = 0, PIS_TD_TERM = 1, PIS_TD_INT = 2 };
+
+__device__ __forceinline__ float pis_horizon(const EqDev& e, float t, float td_dt, bool& td_u) {
+  td_u = td_dt > 0.f && t + td_dt < e.T;
+  return td_u ? td_dt : e.T - t;
+}
+
 template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                      int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
                                                      uint32_t point_base, const float* __restrict__ gx,
-                                                     float* __restrict__ rows, PisRows L) {
+                                                     float* __restrict__ rows, PisRows L, int stage, float td_dt) {
   __shared__ float xsh[NXP_MAX];
   __shared__ float gsts[4 * P * NSG];
   __shared__ float xs3[X3 ? P * (NXP_MAX + 1) : 1];  // split mode: X_s staged [path][dim]
@@ -89,8 +100,11 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
   const uint32_t m = (uint32_t)(m_begin + P * blk + lane);
   const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2;
   const bool TERM = flags & DPI_TERMINAL, INTG = flags & DPI_INTEGRAL;
+  const bool do_term = stage != PIS_TD_INT, do_int = stage != PIS_TD_TERM;
   const float* txr = tx + (size_t)i * F;
-  const float t = txr[0], tmt = e.T - t, Kf = (float)K;
+  const float t = txr[0], Kf = (float)K;
+  bool td_u;
+  const float tmt = pis_horizon(e, t, td_dt, td_u);
   for (int d = tid; d < NXP_MAX; d += NTH) xsh[d] = d < nx ? txr[1 + d] : 0.f;
   const size_t r = (size_t)blockIdx.x * P + lane;
   float* row = rows + r * L.stride;
@@ -103,7 +117,7 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
   float gst[NSG];
 #pragma unroll
   for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
-  for (int j = wv; j < nb; j += 4) {  // terminal path
+  for (int j = wv; do_term && j < nb; j += 4) {  // terminal path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (TERM)
       for (int k = 0; k < K; ++k) {
@@ -120,10 +134,16 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
       if (d < nx) {
         row[L.ST + d] = sv[q];
         if (TERM) Eq<KIND>::gstat(e, d, fmaf(cT, sv[q], xsh[d]), gst);
+        if (stage == PIS_TD_TERM) {  // network input X_{t_next}
+          if (X3)
+            xs3[lane * (NXP_MAX + 1) + d] = fmaf(cT, sv[q], xsh[d]);
+          else
+            row[L.IN + PIS_IN_OFF + d] = fmaf(cT, sv[q], xsh[d]);
+        }
       }
     }
   }
-  for (int j = 3 - wv; j < nb; j += 4) {  // integral path
+  for (int j = 3 - wv; do_int && j < nb; j += 4) {  // integral path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (INTG)
       for (int k = 0; k < K; ++k) {
@@ -146,27 +166,31 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
       }
     }
   }
-  // time embedding of lambda = T - s (each wave writes 16 of the 64 channels)
+  // time embedding of lambda = T - s (each wave writes 16 of the 64 channels); the TD terminal
+  // stage evaluates the network at t_next
+  const float tin = stage == PIS_TD_TERM ? t + td_dt : s;
   if (!X3)
-    for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - s, row + L.E, j);
+    for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - tin, row + L.E, j);
   else if (wv == 0)
-    ssh[lane] = s;
+    ssh[lane] = tin;
 #pragma unroll
   for (int c = 0; c < NSG; ++c) gsts[(wv * P + lane) * NSG + c] = gst[c];
   __syncthreads();
   if (wv == 0) {
     float gT = 0.f;
-    if (TERM) {
+    if (TERM && do_term) {
 #pragma unroll
       for (int c = 0; c < NSG; ++c)
         gst[c] = ((gsts[(0 * P + lane) * NSG + c] + gsts[(1 * P + lane) * NSG + c]) + gsts[(2 * P + lane) * NSG + c]) +
                  gsts[(3 * P + lane) * NSG + c];
       gT = Eq<KIND>::gfin(e, gst);
     }
-    row[L.SC + 0] = s;
-    row[L.SC + 1] = cI;
-    row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
-    row[L.SC + 3] = smt;
+    if (do_int) {
+      row[L.SC + 0] = s;
+      row[L.SC + 1] = cI;
+      row[L.SC + 3] = smt;
+    }
+    if (do_term) row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
   }
   if constexpr (X3) {  // split rows, whole 32-B granule pairs: X_s -> IN chunks 2.., emb -> E
     const int nxc = L.INP / 32 - 2;
@@ -331,19 +355,101 @@ __global__ void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict_
   if (i < n && q == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, A, B);
 }
 
+// TD terminal value (data.py:941-942): for the rows of points with t + td_dt < T, after the
+// forward chain on (t_next, X_{t_next}) rows, a_p = u(t_next, X) - g(x) with
+// u = smooth (net_out . X) + (1 - smooth) g0(e^{-lambda/2} X), lambda = T - t_next
+// (solution.py:256-289).  4 threads per row.
+template <int KIND, bool X3>
+__global__ void k_pis_tvalue(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0, int nbp,
+                             const float* __restrict__ gx, float* __restrict__ rows, PisRows L, int nrows,
+                             float td_dt) {
+  const int r = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
+  const int rc = min(r, nrows - 1);
+  const int g = g0 + rc / P, i = g / nbp;
+  const int nx = e.nx;
+  const float t = tx[(size_t)i * (1 + nx)];
+  bool td_u;
+  (void)pis_horizon(e, t, td_dt, td_u);
+  float* row = rows + (size_t)rc * L.stride;
+  const float lbd = pn.T - (t + td_dt);
+  // smooth (as pis_z_stats)
+  float sr = 0.f;
+  if constexpr (X3) {
+#pragma unroll
+    for (int u = 0; u < PIS_CH / 32; ++u) {
+      float v[8];
+      x3_get8(row, L.H0, u, q, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], v[j], sr);
+    }
+  } else {
+    for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
+  }
+  sr += __shfl_xor(sr, 1, 64);
+  sr += __shfl_xor(sr, 2, 64);
+  const float smooth = sr + pn.snlastb[0] - pn.smooth0;
+  const float decay = __expf(-0.5f * lbd);
+  float sp = 0.f, st[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) st[c] = 0.f;
+  auto visit = [&](int d, float Xd, float nod) {
+    sp = fmaf(nod, Xd, sp);
+    const float y = decay * Xd;
+#pragma unroll
+    for (int c = 0; c < NSG; ++c)
+      if (c < e.ncomp) {
+        const float df = y - e.mean[c * nx + d];
+        st[c] = fmaf(df * df, e.ivar[c * nx + d], st[c]);
+      }
+  };
+  if constexpr (X3) {
+    const int nxc = L.INP / 32 - 2;
+    for (int u = 0; u < nxc; ++u) {
+      float xv[8], nv[8];
+      x3_get8(row, L.IN, 2 + u, q, xv);
+      x3_get8(row, L.NO, u, q, nv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
+        if (d < nx) visit(d, xv[j], nv[j]);
+      }
+    }
+  } else {
+    for (int d = q; d < nx; d += 4) visit(d, row[L.IN + PIS_IN_OFF + d], row[L.NO + d]);
+  }
+  sp += __shfl_xor(sp, 1, 64);
+  sp += __shfl_xor(sp, 2, 64);
+  float lp[NSG], mx = -3.0e38f;
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) {
+    st[c] += __shfl_xor(st[c], 1, 64);
+    st[c] += __shfl_xor(st[c], 2, 64);
+    lp[c] = c < e.ncomp ? e.logc[c] - 0.5f * st[c] : -3.0e38f;
+    mx = fmaxf(mx, lp[c]);
+  }
+  float ws = 0.f;
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) ws += c < e.ncomp ? __expf(lp[c] - mx) : 0.f;
+  const float g0v = -(mx + __logf(ws));  // g0 = -log p (equations.py:592-593)
+  const float u = smooth * sp + (1.0f - smooth) * g0v;
+  if (r < nrows && q == 0 && td_u) row[L.SC + 2] = u - gx[i];
+}
+
 // Per-path f, b_p and label contributions for one (point, 64-path block) -> partial slab.
 template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                    int nbp, int K, int flags, const float* __restrict__ fbv,
                                                    const float* __restrict__ rows, PisRows L,
-                                                   float* __restrict__ partial) {
+                                                   float* __restrict__ partial, float td_dt) {
   __shared__ float cs[2][P][NXP_MAX + 4];  // per-path contributions and their squares: [path][col]
   const int tid = threadIdx.x;
   const int g = g0 + blockIdx.x;
   const int i = g / nbp, b = g - i * nbp;
   const int nx = e.nx, F = 1 + nx;
   const bool TERM = flags & DPI_TERMINAL, INTG = flags & DPI_INTEGRAL;
-  const float t = tx[(size_t)i * F], tmt = e.T - t, Kf = (float)K;
+  const float t = tx[(size_t)i * F], Kf = (float)K;
+  bool td_u;
+  const float tmt = pis_horizon(e, t, td_dt, td_u);  // horizon (TD: t_next - t)
   const float f_b = fbv[i];
   const int p = tid >> 2, q = tid & 3;
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;

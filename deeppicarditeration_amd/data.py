@@ -17,7 +17,7 @@ Differences from the reference, by design:
   the fp64 reference, tests/test_gpu_parity.py).
 
 `estimate_delta_t > 0` selects the reference's TD estimators (data.py:1209-1213) on the device
-(MLP and zero networks).
+(every network kind).
 """
 from typing import Union
 

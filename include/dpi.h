@@ -98,8 +98,9 @@ int dpi_problem_set_hessian_approximation(dpi_problem p, int sdgd_v);
  * (estimate_terminal_with_gradients_td, estimate_integral_with_gradients_td): per point the
  * horizon is t_next = min(t + delta_t, T) instead of T, s ~ U(t, t_next], and the terminal value
  * is u(t_next, X_{t_next}) (the network) where t_next < T, g(X_T) otherwise.  0 (default) = the
- * plain estimators.  MLP and zero networks (PISGradNet: DPI_ERR_UNSUPPORTED); the Hessian-label
- * entry points ignore it, as the reference's generate_with_gradients_and_hessians does. */
+ * plain estimators.  Every network kind (PISGradNet: a terminal stage — rollout to t_next, forward
+ * GEMM chain, u — before the integral stage); the Hessian-label entry points ignore it, as the
+ * reference's generate_with_gradients_and_hessians does. */
 int dpi_problem_set_estimate_delta_t(dpi_problem p, double delta_t);
 int dpi_problem_destroy(dpi_problem p);
 

@@ -26,8 +26,7 @@ from golden_util import CASES, delta_t, load, oracle_equation, oracle_net  # noq
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
-# TD estimators with PISGradNet are not built (dpi_problem_set_estimate_delta_t): they raise
-SUPPORTED = [c for c in CASES if not (c.startswith("td_") and "pis" in c)]
+SUPPORTED = list(CASES)
 
 
 @pytest.mark.parametrize("case", SUPPORTED)
@@ -94,13 +93,33 @@ def test_td_terminal_and_integral_estimators(case):
     assert pI["value"] < TOL and pI["grad"] < TOL, pI
 
 
-def test_td_pisgradnet_fails_loudly():
-    from deeppicarditeration_amd._lib import DPIError
-    f = load("td_ou_pis32_K2")
-    eq = product_equation(f)
-    gen = generator(f, eq, product_module(f, eq))
-    with pytest.raises(DPIError):
-        gen.generate_with_gradients(torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0"))
+@pytest.mark.parametrize("gemm_mode", [0, 1])
+def test_td_pisgradnet_config3_network_vs_oracle(gemm_mode):
+    """TD estimators with PISGradNet 4x512 (config-3 network): terminal stage (rollout to t_next,
+    forward GEMM chain, u(t_next, X)) then the integral stage, vs the oracle; fp32 and
+    fp16-split GEMMs."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    L.check(L.load().dpi_set_gemm_precision(gemm_mode), "gemm precision")
+    try:
+        eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+        torch.manual_seed(3)
+        net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+        M, K, n, dt = 128, 10, 8, 0.4
+        gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                      n_estimate_integral=M, n_euler_steps=K, seed=2, estimate_delta_t=dt)
+        tx, _ = gen.sample_t_and_x(n, point_base=0)
+        t = tx[:, 0].cpu().numpy()
+        assert (t + dt < 1).any() and (t + dt >= 1).any()
+        y = gen.generate_with_gradients(tx, point_base=0).cpu().numpy()
+    finally:
+        L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "gemm precision")
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), M, K, 2, 1, 0, delta_t=dt)
+    parts = rel_l2_parts(y, ref)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
 def test_td_generator_does_not_leak_into_shared_problem():
