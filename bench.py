@@ -200,6 +200,25 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, k_ms = float(t[0]), float(t[1])
     assert torch.isfinite(y).all()
+    # Noise floor of the same launch (untimed, after the timed region): the identical rollout with
+    # u = 0 (ZeroSolution: same Philox streams, same K-step EM, no network), i.e. the
+    # Philox4x32-10 + Box-Muller VALU issue the noise contract fixes.
+    floor_ms = None
+    if rank == 0 and not wl.get("pis") and not wl.get("hess"):
+        gen0 = dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(1), 80, 1, device=dev, t_always_uniform=True,
+                                       n_estimate_terminal=M_PER_GPU, n_estimate_integral=M_PER_GPU,
+                                       n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
+        tx0, pb0 = gen0.sample_t_and_x(N_POINTS)
+        ws0 = gen0.point_baseline(tx0)
+        fl = []
+        for it in range(8):
+            f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            f0.record()
+            gen0.label_moments(tx0, pb0, M_PER_GPU, 0, M_PER_GPU, L.DPI_BOTH, ws0)
+            f1.record()
+            fl.append((f0, f1))
+        torch.cuda.synchronize()
+        floor_ms = sum(a.elapsed_time(b) for a, b in fl[2:]) / len(fl[2:])
     path_labels_per_step = N_POINTS * M  # all ranks together
     value = path_labels_per_step * args.steps / dt
     if rank == 0:
@@ -232,6 +251,11 @@ def main():
                          "kernel": wl["kernel"],
                          "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
         }
+        if floor_ms is not None:
+            out["roofline"]["noise_floor"] = {
+                "what": "same launch with u = 0 (ZeroSolution): Philox4x32-10 + Box-Muller + K-step EM only, the "
+                        "VALU-issue floor of the noise contract (2 x K x nx normals per path-label)",
+                "kernel_ms": floor_ms, "frac": floor_ms / k_ms}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_paths if args.workload == "burgers" else 64)
         print(json.dumps(out), flush=True)
