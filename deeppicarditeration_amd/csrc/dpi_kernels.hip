@@ -148,6 +148,34 @@ static int upload(dpi_problem_s* p, const std::vector<T>& v, const T** out) {
   return 0;
 }
 
+// The same fragment order for the split-storage GEMM (k_gemm_x3, dpi_gemm.h): x' = 2^s x with
+// max |x'| in [0.5, 1), hi = fp16(x'), lo = fp16(x' - hi) (unscaled).  *wscale = 2^-s.
+template <class F>
+static size_t pack_split_x3(std::vector<float>& blob, int R, int C, F at, float* wscale) {
+  float mx = 0.f;
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < C; ++c) mx = std::max(mx, std::fabs(at(r, c)));
+  int e = 0;
+  if (mx > 0.f) (void)std::frexp(mx, &e);  // mx = f 2^e, f in [0.5, 1)
+  const float sc = std::ldexp(1.0f, -e);
+  *wscale = std::ldexp(1.0f, e);
+  const size_t off = blob.size();
+  blob.resize(off + (size_t)R * C, 0.f);
+  _Float16* dst = reinterpret_cast<_Float16*>(blob.data() + off);
+  for (int r = 0; r < R; ++r)
+    for (int u = 0; u < C / 32; ++u)
+      for (int q = 0; q < 4; ++q) {
+        _Float16* g = dst + ((size_t)r * C + 32 * u + 8 * q) * 2;  // 16 halves = 8 words
+        for (int j = 0; j < 8; ++j) {
+          const float x = at(r, 32 * u + 4 * q + (j & 3) + 16 * (j >> 2)) * sc;
+          const _Float16 h = (_Float16)x;
+          g[j] = h;
+          g[8 + j] = (_Float16)(x - (float)h);
+        }
+      }
+  return off;
+}
+
 // Append an R x C (C % 32 == 0) matrix in the fp16-split fragment order of mlp_tile_split:
 // row r, chunk u, lane group q: 8 hi halves then 8 lo halves of columns 32u + 4q + (j & 3) + 16 (j >> 2).
 // Returns the offset (in 4-byte words) into `blob`.
@@ -516,33 +544,34 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
   int hp[4];
   for (int l = 0; l < L; ++l) hp[l] = r64(hidden[l]);
   size_t s_te0, s_te2, s_sn0, s_sn[4] = {0}, s_nn[5] = {0}, s_nnT[5] = {0}, s_nnbP[5] = {0};
+  float w_te0 = 1.f, w_te2 = 1.f, w_sn0 = 1.f, w_sn[4] = {1.f, 1.f, 1.f, 1.f}, w_nn[5], w_nnT[5];
   {
     auto align = [&]() { blob.resize((blob.size() + 31) & ~size_t(31), 0.f); };
-    auto packm = [&](const float* src, int rows, int cols, int Np, int Kp, bool trans) {
+    auto packm = [&](const float* src, int rows, int cols, int Np, int Kp, bool trans, float* ws) {
       align();
-      return pack_split(blob, Np, Kp, [&](int r, int c) {
+      return pack_split_x3(blob, Np, Kp, [&](int r, int c) {
         if (trans) return (c < rows && r < cols) ? src[(size_t)c * cols + r] : 0.f;  // (src^T)[r][c]
         return (r < rows && c < cols) ? src[(size_t)r * cols + c] : 0.f;
-      });
+      }, ws);
     };
-    s_te0 = packm(te0, C, 2 * C, C, 2 * C, false);
-    s_te2 = packm(te2, C, C, C, C, false);
-    s_sn0 = packm(sn0, C, 2 * C, C, 2 * C, false);
-    for (int j = 0; j < nsm; ++j) s_sn[j] = packm(snw[j], C, C, C, C, false);
+    s_te0 = packm(te0, C, 2 * C, C, 2 * C, false, &w_te0);
+    s_te2 = packm(te2, C, C, C, C, false, &w_te2);
+    s_sn0 = packm(sn0, C, 2 * C, C, 2 * C, false, &w_sn0);
+    for (int j = 0; j < nsm; ++j) s_sn[j] = packm(snw[j], C, C, C, C, false, &w_sn[j]);
     // forward: nn[0] (h0 x (64 + nx)), nn[l] (h_l x h_{l-1}), nn[L] (nx x h_{L-1})
-    s_nn[0] = packm(nnw[0], hidden[0], ins[0], hp[0], INP, false);
-    for (int l = 1; l < L; ++l) s_nn[l] = packm(nnw[l], hidden[l], ins[l], hp[l], hp[l - 1], false);
-    s_nn[L] = packm(nnw[L], nx, ins[L], NOP, hp[L - 1], false);
+    s_nn[0] = packm(nnw[0], hidden[0], ins[0], hp[0], INP, false, &w_nn[0]);
+    for (int l = 1; l < L; ++l) s_nn[l] = packm(nnw[l], hidden[l], ins[l], hp[l], hp[l - 1], false, &w_nn[l]);
+    s_nn[L] = packm(nnw[L], nx, ins[L], NOP, hp[L - 1], false, &w_nn[L]);
     // VJP: nnT[L] = nn[L]^T (h_{L-1} x nx), nnT[l] = nn[l]^T, nnT[0] = nn[0][:, 64:]^T (nx x h0)
-    s_nnT[L] = packm(nnw[L], nx, ins[L], hp[L - 1], NXK, true);
-    for (int l = 1; l < L; ++l) s_nnT[l] = packm(nnw[l], hidden[l], ins[l], hp[l - 1], hp[l], true);
+    s_nnT[L] = packm(nnw[L], nx, ins[L], hp[L - 1], NXK, true, &w_nnT[L]);
+    for (int l = 1; l < L; ++l) s_nnT[l] = packm(nnw[l], hidden[l], ins[l], hp[l - 1], hp[l], true, &w_nnT[l]);
     {
       align();
       const float* w0 = nnw[0];
       const int in0 = ins[0], h0 = hidden[0];
-      s_nnT[0] = pack_split(blob, NOP, hp[0], [&](int d, int h) {
+      s_nnT[0] = pack_split_x3(blob, NOP, hp[0], [&](int d, int h) {
         return (d < nx && h < h0) ? w0[(size_t)h * in0 + C + d] : 0.f;
-      });
+      }, &w_nnT[0]);
     }
     for (int l = 0; l <= L; ++l) {
       const int o = l < L ? hidden[l] : nx, op = l < L ? hp[l] : NOP;
@@ -592,10 +621,13 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
     pd.te0S = u32(s_te0);
     pd.te2S = u32(s_te2);
     pd.sn0S = u32(s_sn0);
-    for (int j = 0; j < nsm; ++j) pd.snS[j] = u32(s_sn[j]);
+    pd.te0W = w_te0, pd.te2W = w_te2, pd.sn0W = w_sn0;
+    for (int j = 0; j < nsm; ++j) pd.snS[j] = u32(s_sn[j]), pd.snW[j] = w_sn[j];
     for (int l = 0; l <= L; ++l) {
       pd.nnS[l] = u32(s_nn[l]);
       pd.nnTS[l] = u32(s_nnT[l]);
+      pd.nnW[l] = w_nn[l];
+      pd.nnTW[l] = w_nnT[l];
       pd.nnbP[l] = base + s_nnbP[l];
     }
   }
@@ -726,24 +758,28 @@ static void gemm(int epi, int M, int N, int K, const float* A, int lda, const fl
 
 // Split-storage GEMM: OUT (M x Np) = epi(X (M x Kp) W^T), all split (Np, Kp multiples of 32).
 template <int NT>
-static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, const float* X, int ldx, float* OUT, int ldc,
-                       const float* bias, const float* aux, int ldaux, hipStream_t st) {
+static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
+                       float* OUT, int ldc, const float* bias, const float* aux, int ldaux, hipStream_t st) {
   const int nnt = Np / (32 * NT), nmt = (M + X3_BM - 1) / X3_BM;
   dim3 grid(nnt * nmt), block(X3_THREADS);
   if (epi == EPI_BIAS)
-    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, X, ldx, OUT, ldc, bias, aux, ldaux);
-  else if (epi == EPI_BIAS_ELU)
-    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, X, ldx, OUT, ldc, bias, aux,
+    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias, aux,
                        ldaux);
+  else if (epi == EPI_BIAS_ELU)
+    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias,
+                       aux, ldaux);
   else
-    hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, X, ldx, OUT, ldc, bias, aux, ldaux);
+    hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias, aux,
+                       ldaux);
 }
-static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, const float* X, int ldx, float* OUT, int ldc,
-                    const float* bias, const float* aux, int ldaux, hipStream_t st) {  // Np % 64 == 0, Kp % 32 == 0
+// ws: the weight matrix's scale 2^-s (pack_split_x3)
+static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx, float* OUT,
+                    int ldc, const float* bias, const float* aux, int ldaux,
+                    hipStream_t st) {  // Np % 64 == 0, Kp % 32 == 0
   if (Np % 128 == 0)
-    gemm_x3_nt<4>(epi, M, Kp, Np, W, X, ldx, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<4>(epi, M, Kp, Np, W, ws, X, ldx, OUT, ldc, bias, aux, ldaux, st);
   else
-    gemm_x3_nt<2>(epi, M, Kp, Np, W, X, ldx, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, OUT, ldc, bias, aux, ldaux, st);
 }
 
 // The PISGradNet chain of pis_chain in split storage (every width padded to 32; the x part of IN
@@ -752,34 +788,34 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   PisRows L = pis_rows_layout(pd, true);
   auto r64 = [](int x) { return (x + 63) & ~63; };
   const int ld = L.stride, C = PIS_CH, NXK = (pd.nx + 31) & ~31, NOP = r64(pd.nx);
-  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.te0S, rows + L.E, ld, rows + L.T1, ld, pd.te0b, nullptr, 0, st);
-  gemm_x3(EPI_BIAS, R, C, C, pd.te2S, rows + L.T1, ld, rows + L.IN, ld, pd.te2b, nullptr, 0, st);
+  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.te0S, pd.te0W, rows + L.E, ld, rows + L.T1, ld, pd.te0b, nullptr, 0, st);
+  gemm_x3(EPI_BIAS, R, C, C, pd.te2S, pd.te2W, rows + L.T1, ld, rows + L.IN, ld, pd.te2b, nullptr, 0, st);
   int hs = L.H0, ho = L.H1;
-  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.sn0S, rows + L.E, ld, rows + hs, ld, pd.sn0b, nullptr, 0, st);
+  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.sn0S, pd.sn0W, rows + L.E, ld, rows + hs, ld, pd.sn0b, nullptr, 0, st);
   for (int j = 0; j < pd.nsm; ++j) {
-    gemm_x3(EPI_BIAS_ELU, R, C, C, pd.snS[j], rows + hs, ld, rows + ho, ld, pd.snb[j], nullptr, 0, st);
+    gemm_x3(EPI_BIAS_ELU, R, C, C, pd.snS[j], pd.snW[j], rows + hs, ld, rows + ho, ld, pd.snb[j], nullptr, 0, st);
     std::swap(hs, ho);
   }
   int Kp = L.INP;
   const float* a = rows + L.IN;
   for (int l = 0; l < pd.L; ++l) {
-    gemm_x3(EPI_BIAS_ELU, R, Kp, r64(pd.h[l]), pd.nnS[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, st);
+    gemm_x3(EPI_BIAS_ELU, R, Kp, r64(pd.h[l]), pd.nnS[l], pd.nnW[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, st);
     a = rows + L.A[l];
     Kp = r64(pd.h[l]);
   }
-  gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
+  gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
   L.H0 = hs;
   if (!vjp) return L;
   // VJP: the x part of IN starts at its chunk 2 (word 64)
   int dcur = L.D0, dnext = L.D1;
-  gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld, nullptr,
+  gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], pd.nnTW[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld, nullptr,
           rows + L.A[pd.L - 1], ld, st);
   for (int l = pd.L - 1; l >= 1; --l) {
-    gemm_x3(EPI_DELU, R, r64(pd.h[l]), r64(pd.h[l - 1]), pd.nnTS[l], rows + dcur, ld, rows + dnext, ld, nullptr,
+    gemm_x3(EPI_DELU, R, r64(pd.h[l]), r64(pd.h[l - 1]), pd.nnTS[l], pd.nnTW[l], rows + dcur, ld, rows + dnext, ld, nullptr,
             rows + L.A[l - 1], ld, st);
     std::swap(dcur, dnext);
   }
-  gemm_x3(EPI_BIAS, R, r64(pd.h[0]), NOP, pd.nnTS[0], rows + dcur, ld, rows + L.GX, ld, nullptr, nullptr, 0, st);
+  gemm_x3(EPI_BIAS, R, r64(pd.h[0]), NOP, pd.nnTS[0], pd.nnTW[0], rows + dcur, ld, rows + L.GX, ld, nullptr, nullptr, 0, st);
   L.H0 = hs;
   return L;
 }

@@ -41,6 +41,8 @@ struct NetPisDev {
   const uint32_t *te0S, *te2S, *sn0S, *snS[4];
   const uint32_t *nnS[5], *nnTS[5];
   const float* nnbP[5];
+  // k_gemm_x3 weight scales 2^-s (each split matrix is stored prescaled by 2^s)
+  float te0W, te2W, sn0W, snW[4], nnW[5], nnTW[5];
 };
 
 __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float* out /* stride 1 */, int j) {

@@ -501,7 +501,7 @@ void report_u(const char* name, int M, int Kp, int Np, const uint32_t* W, float 
           const _Float16 l = __builtin_bit_cast(_Float16, (uint16_t)((j & 1) ? lw >> 16 : lw & 0xFFFF));
           return (double)(float)h + (double)(float)l * lsc;
         };
-        const double x = dec(a, 1.0), y = dec(b, 1.0 / 2048.0);
+        const double x = dec(a, 1.0), y = dec(b, 1.0);
         maxrel = std::fmax(maxrel, std::fabs(x - y));
         maxref = std::fmax(maxref, std::fabs(y));
       }
@@ -602,50 +602,39 @@ int main() {
   for (int i = 0; i < Np; ++i) hb[i] = 0.01f * (float)((i * 37) % 17 - 8);
   CK(hipMemcpy(bias, hb.data(), Np * 4, hipMemcpyHostToDevice));
   CK(hipDeviceSynchronize());
-  // reference outputs: the product kernel (dpi_gemm.h)
+  // reference outputs: the product kernel (dpi_gemm.h, unscaled-lo split, weights prescaled 2^4)
   const int nnt = Np / 128, nmt = M / X3_BM;
+  auto prod = [&](int epi, int iters) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) {
+      if (epi == 1)
+        hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
+                           1.0f / 16.0f, XU, Kp, REF, Np, bias, AUXU, Np);
+      else
+        hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
+                           1.0f / 16.0f, XU, Kp, REF, Np, nullptr, AUXU, Np);
+    }
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e3f / iters;
+  };
   for (int epi = 1; epi <= 2; ++epi) {
-    if (epi == 1)
-      hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, W, X, Kp,
-                         REF, Np, bias, AUX, Np);
-    else
-      hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, W, X, Kp, REF,
-                         Np, nullptr, AUX, Np);
-    CK(hipDeviceSynchronize());
+    prod(epi, 1);
+    const float us = prod(epi, 50);
+    std::printf("%s product k_gemm_x3               %8.2f us  %7.1f TF/s(eff f16)\n", epi == 1 ? "elu " : "delu", us,
+                2.0 * 3.0 * M * (double)Kp * Np / (us * 1e-6) / 1e12);
+    prod(epi, 1);  // REF = product output
     if (epi == 1) {
-      report<EPI_BIAS_ELU, 4, 0>("elu  v0 (product copy)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
-      report<EPI_BIAS_ELU, 4, 1>("elu  v1 (no epilogue)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
-      report<EPI_BIAS_ELU, 4, 4>("elu  v4 (group swizzle)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
-      report<EPI_BIAS_ELU, 4, 5>("elu  v5 (group swizzle, no epi)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
-      report_u<EPI_BIAS_ELU, 0>("elu  W2 (1 acc, pipelined frags)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias,
-                                AUXU);
-      report_u<EPI_BIAS_ELU, 1>("elu  W2 no epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
-      {  // per-wave cycle stamps of the W2 main loop (no epilogue), averaged over all waves
-        unsigned long long* st;
-        const int nblk = (Np / 128) * (M / X3_BM);
-        CK(hipMalloc(&st, (size_t)nblk * 8 * 8 * 8));
-        hipLaunchKernelGGL((k_x3u<EPI_BIAS_ELU, 65>), dim3(nblk), dim3(X3_THREADS), 0, 0, M, Kp, Np / 128, WU,
-                           1.0f / 16.0f, XU, Kp, OUT, Np, bias, reinterpret_cast<const float*>(st), Np);
-        CK(hipDeviceSynchronize());
-        std::vector<unsigned long long> h((size_t)nblk * 64);
-        CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-        double a[6] = {0, 0, 0, 0, 0, 0};
-        for (int w = 0; w < nblk * 8; ++w)
-          for (int k = 0; k < 6; ++k) a[k] += (double)h[(size_t)w * 8 + k] / (nblk * 8);
-        std::printf("W2 stamps per wave (cycles): lgkm %.0f  vmcnt %.0f  barrier %.0f  issue+frag %.0f  mma-issue %.0f"
-                    "  total %.0f\n", a[0], a[1], a[2], a[3], a[4], a[5]);
-        CK(hipFree(st));
-      }
-      report_u<EPI_BIAS_ELU, 128>("elu  W3 (branch-free, interleaved)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
-                                  bias, AUXU);
+      report<EPI_BIAS_ELU, 4, 1>("elu  v1 (old loop, no epilogue)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
+      report_u<EPI_BIAS_ELU, 128>("elu  W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
       report_u<EPI_BIAS_ELU, 129>("elu  W3 no epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
     } else {
-      report<EPI_DELU, 4, 0>("delu v0 (product copy)", M, Kp, Np, W, X, OUT, REF, nullptr, AUX);
-      report<EPI_DELU, 4, 4>("delu v4 (group swizzle)", M, Kp, Np, W, X, OUT, REF, nullptr, AUX);
-      report_u<EPI_DELU, 0>("delu W2 (1 acc, pipelined frags)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, nullptr,
-                            AUXU);
-      report_u<EPI_DELU, 128>("delu W3 (branch-free, interleaved)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
-                              nullptr, AUXU);
+      report_u<EPI_DELU, 128>("delu W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, nullptr, AUXU);
     }
   }
   std::printf("done\n");
