@@ -28,26 +28,33 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 NX = 100
-PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector peak
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector peak (v_mfma_f32_16x16x4_f32)
+PEAK_F16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense MFMA peak
+# fp16-split MFMA (include/dpi.h DPI_GEMM_F16X3, the default): one fp32 product = 3 f16 products
+PEAK_SPLIT_TFLOPS = PEAK_F16_TFLOPS / 3.0
 PEAK_HBM_GBS = 8000.0
-# workloads = BASELINE.json configs; FLOP per path-label from SURVEY.md §8(d)
+# workloads = BASELINE.json configs; FLOP per path-label from SURVEY.md §8(d), except GBM, whose
+# kernel runs a cheaper algorithm than §8(d) assumes (adjoint + first-order tangents instead of
+# second-order forward mode): there the FLOPs it executes are counted.
+# "peak": the MFMA the kernel's network evaluation runs on.
 WORKLOADS = {
     "burgers": dict(cfg="configs[1]", eq="Cha", widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0,
-                    flop=2.72e5, kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
+                    flop=2.72e5, peak="split", kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
                                       "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)"),
     "hjb": dict(cfg="configs[2]", eq="OUProcessEquation", widths=[512] * 4, pis=True, points=64, m_per_gpu=4096, K=50,
-                sdgd=0, flop=3.73e6, kernel="k_pis_rollout + k_gemm_nt chain + k_pis_final + k_reduce per "
-                                            "dpi_label_moments call",
+                sdgd=0, flop=3.73e6, peak="split", kernel="k_pis_rollout + k_gemm_x3 chain (fp16-split) + "
+                                                           "k_pis_final + k_reduce per dpi_label_moments call",
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
                      "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
     "gbm_hess": dict(cfg="configs[4] stretch (Malliavin Hessian labels)", eq="GBMEquationComplexExact", widths=[64] * 3,
-                     points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6,
+                     points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6, peak="f32",
                      kernel="k_paths<GBM,64,3,hessians> + k_reduce + k_reduce_hess per dpi_label_moments_hessians call",
                      desc="Fully-nonlinear case_1 100d (GBM), generate_with_gradients_and_hessians: labels "
                           "(u, u_x, u_xx) = 1 + 100 + 10,000 wide, full-Hessian f at 3 points per path, 64 points x "
                           "1024 MC paths per GPU, K=50, MLP 101-64x3-1 ELU"),
     "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
-                sdgd=100, flop=3.36e6, kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
+                sdgd=100, flop=1.68e6, survey_flop=3.36e6, peak="f32",
+                kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
                 desc="Fully-nonlinear case_1 100d (GBM, SDGD v=100), 64 points x 1024 MC paths per GPU, K=50, "
                      "MLP 101-64x3-1 ELU (BASELINE configs[4])"),
 }
@@ -224,6 +231,13 @@ def main():
     if rank == 0:
         per_launch_units = N_POINTS * M_PER_GPU
         achieved = FLOP_PER_PATH_LABEL * per_launch_units / (k_ms * 1e-3) / 1e12
+        if wl["peak"] == "split":
+            peak = PEAK_SPLIT_TFLOPS
+            peak_basis = ("fp32-equivalent peak of the fp16-split MFMA the network runs on: 2.5 PFLOP/s dense f16 "
+                          "(v_mfma_f32_16x16x32_f16) / 3 f16 products per fp32 product")
+        else:
+            peak = PEAK_FP32_TFLOPS
+            peak_basis = "fp32 MFMA (v_mfma_f32_16x16x4_f32) = fp32 vector peak"
         traffic = None
         tf = ROOT / "profiles" / f"traffic_{args.workload}.json"
         if tf.exists():
@@ -246,11 +260,13 @@ def main():
                        "parallelism": f"mc-shard{world}", "per_gpu_value": value / world,
                        "prewarm_steps": prewarm,
                        "rel_l2_vs_ref": "<= 3e-7 measured, tolerance 1e-4 (tests/test_gpu_parity.py)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "kernel": wl["kernel"],
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
+                         "peak_basis": peak_basis, "kernel": wl["kernel"],
                          "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
         }
+        if "survey_flop" in wl:
+            out["roofline"]["survey_flop_per_path_label"] = wl["survey_flop"]
         if floor_ms is not None:
             out["roofline"]["noise_floor"] = {
                 "what": "same launch with u = 0 (ZeroSolution): Philox4x32-10 + Box-Muller + K-step EM only, the "
