@@ -47,13 +47,13 @@ WORKLOADS = {
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
                      "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
     "gbm_hess": dict(cfg="configs[4] stretch (Malliavin Hessian labels)", eq="GBMEquationComplexExact", widths=[64] * 3,
-                     points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6, peak="f32",
+                     points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6, peak="split",
                      kernel="k_paths<GBM,64,3,hessians> + k_reduce + k_reduce_hess per dpi_label_moments_hessians call",
                      desc="Fully-nonlinear case_1 100d (GBM), generate_with_gradients_and_hessians: labels "
                           "(u, u_x, u_xx) = 1 + 100 + 10,000 wide, full-Hessian f at 3 points per path, 64 points x "
                           "1024 MC paths per GPU, K=50, MLP 101-64x3-1 ELU"),
     "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
-                sdgd=100, flop=1.68e6, survey_flop=3.36e6, peak="f32",
+                sdgd=100, flop=1.68e6, survey_flop=3.36e6, peak="split",
                 kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
                 desc="Fully-nonlinear case_1 100d (GBM, SDGD v=100), 64 points x 1024 MC paths per GPU, K=50, "
                      "MLP 101-64x3-1 ELU (BASELINE configs[4])"),

@@ -735,6 +735,164 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
   s2_out = s2;
 }
 
+// mlp_hdiag on the fp16-split MFMA (H % 32 == 0): same inputs and outputs.  The hidden layers'
+// split weights (NetDev::WS, fragment order) are loaded ONCE into registers as MFMA A fragments
+// (2 (L - 1) (H / 16) (H / 32) half8 pairs: 128 VGPRs at H = 64, L = 3) and reused by the forward
+// pass and by every direction of the tangent sweep, which then runs without LDS traffic: per
+// direction and layer (H/16)(H/32) x 3 v_mfma_f32_16x16x32_f16 instead of (H/16)(H/4)
+// v_mfma_f32_16x16x4_f32 (5.3x fewer MFMA cycles); the tangent / activation B operands are split
+// in registers.  Layer 0 (the noise tile through W1x) and the z_0 = W1x[:, d] lookups stay fp32
+// from LDS; the adjoint reads the transposed split weights (WTS) from L2 once.
+template <int H, int L>
+__device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
+                                                float& s1_out, float& s2_out) {
+  static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
+  constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
+  constexpr int WXS = LdsGbm<H>::WXS;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int jj = lane & 15, qq = lane >> 4;
+  const int pp = 16 * wv + jj;
+  const float tau = sh.tau[pp];
+  const float cm = sh.cmul[pp];
+  auto afrag = [&](const uint32_t* W, int row, int u, half8& ah, half8& al) {  // global, fragment order
+    const uint32_t* rp = W + (size_t)row * H + 4 * (8 * u + 2 * qq);
+    ah = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp));
+    al = __builtin_bit_cast(half8, *reinterpret_cast<const u32v4*>(rp + 4));
+  };
+  half8 wh[LH][HT][NU], wl[LH][HT][NU];
+#pragma unroll
+  for (int l = 1; l < L; ++l)
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) afrag(net.WS[l], 16 * T + jj, u, wh[l - 1][T][u], wl[l - 1][T][u]);
+  // o = W_l B for the B operand (bh, bl) split per chunk, from the register-resident fragments
+  auto wmul = [&](int l, const half8 (&bh)[NU], const half8 (&bl)[NU], floatx4 (&o)[HT]) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 am = {0.f, 0.f, 0.f, 0.f}, ac = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        am = mfma16(wh[l - 1][T][u], bh[u], am);
+        ac = mfma16(wh[l - 1][T][u], bl[u], ac);
+        ac = mfma16(wl[l - 1][T][u], bh[u], ac);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
+    }
+  };
+  float act[L][HT][4];
+  float lam[L][HT][4];
+  // forward, layer 0: fp32 MFMA over the noise tile (once per path)
+#pragma unroll
+  for (int T = 0; T < HT; ++T) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    for (int t = 0; t < nxt; ++t) {
+      const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+      const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
+      acc = mfma4(a.x, bc[0], acc);
+      acc = mfma4(a.y, bc[SS], acc);
+      acc = mfma4(a.z, bc[2 * SS], acc);
+      acc = mfma4(a.w, bc[3 * SS], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * T + 4 * qq + r;
+      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+    }
+  }
+  // hidden layers (split MFMA)
+#pragma unroll
+  for (int l = 1; l < L; ++l) {
+    half8 bh[NU], bl[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(act[l - 1][2 * u], act[l - 1][2 * u + 1], bh[u], bl[u]);
+    floatx4 o[HT];
+    wmul(l, bh, bl, o);
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(o[T][r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+  }
+  // adjoints lam_l = du/da_l: lam_l = W_{l+1}^T (elu'(a_{l+1}) lam_{l+1})
+#pragma unroll
+  for (int T = 0; T < HT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lam[L - 1][T][r] = sh.vec[2 * H + 16 * T + 4 * qq + r];
+#pragma unroll
+  for (int l = L - 2; l >= 0; --l) {
+    float Bm[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l + 1][t][r]) * lam[l + 1][t][r];
+    half8 bh[NU], bl[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) split_act(Bm[2 * u], Bm[2 * u + 1], bh[u], bl[u]);
+#pragma unroll
+    for (int T = 0; T < HT; ++T) {
+      floatx4 am = {0.f, 0.f, 0.f, 0.f}, ac = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        half8 ah, al;
+        afrag(net.WTS[l + 1], 16 * T + jj, u, ah, al);
+        am = mfma16(ah, bh[u], am);
+        ac = mfma16(ah, bl[u], ac);
+        ac = mfma16(al, bh[u], ac);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lam[l][T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
+    }
+  }
+  // lam_l elu''(a_l): the per-layer weights of the squared tangents
+#pragma unroll
+  for (int l = 0; l < L; ++l)
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lam[l][T][r] *= d2elu_from_a(act[l][T][r]);
+  // tangent sweep over the state dimensions
+  float s1 = 0.f, s2 = 0.f;
+  for (int d = 0; d < e.nx; ++d) {
+    float z[HT][4];
+    float term = 0.f;
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+        term = fmaf(lam[0][T][r], z[T][r] * z[T][r], term);
+      }
+#pragma unroll
+    for (int l = 1; l < L; ++l) {
+      float Bm[HT][4];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l - 1][t][r]) * z[t][r];
+      half8 bh[NU], bl[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) split_act(Bm[2 * u], Bm[2 * u + 1], bh[u], bl[u]);
+      floatx4 o[HT];
+      wmul(l, bh, bl, o);
+#pragma unroll
+      for (int T = 0; T < HT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          z[T][r] = o[T][r];
+          term = fmaf(lam[l][T][r], o[T][r] * o[T][r], term);
+        }
+    }
+    const float ud = qsum(term);
+    const float c = (float)sh.cnt[d * P + pp];
+    s1 = fmaf(c, ud, s1);
+    s2 = fmaf(c, fabsf(ud), s2);
+  }
+  s1_out = s1;
+  s2_out = s2;
+}
+
 // u(tau, x + cmul S) for this wave's 16 paths with every weight LDS-resident (GBM layout):
 // the forward half of mlp_hdiag.  The TD terminal value (data.py:941-942).
 template <int H, int L>
@@ -1078,7 +1236,7 @@ __device__ __forceinline__ void hess_accum(LdsGbm<H>& sh, const float* wgt, int 
   }
 }
 
-template <int KIND, int H, int L, bool ZERO>
+template <int KIND, int H, int L, bool ZERO, bool SPLIT>
 __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, const PathArgs& a, LdsGbm<H>& sh,
                                            int i, int blk, uint32_t ig, uint32_t m, float s, float smt, float tmt,
                                            float g_x, int nxp) {
@@ -1088,7 +1246,12 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
   // valid in the lanes of group qq == 0 for path pp
   auto f_eval = [&]() -> float {
     float s1 = 0.f, s2 = 0.f;
-    if (!ZERO) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+    if constexpr (!ZERO) {
+      if constexpr (SPLIT)
+        mlp_hdiag_split<H, L>(e, net, sh, nxp / 16, s1, s2);
+      else
+        mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+    }
     const float c1 = 0.5f * (1.0f - e.alpha), c2 = 0.25f;
     float arg[NSG], sn[NSG];
     const float spp = sh.tau[pp], cpp = sh.cmul[pp];
@@ -1432,7 +1595,14 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       // gathers the point's Hessian diagonal at this path's indices (data.py:1293-1302).
       const int jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
       float s1 = 0.f, s2 = 0.f;
-      if (!ZERO && INTG) mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+      if constexpr (!ZERO) {
+        if (INTG) {
+          if constexpr (SPLIT)
+            mlp_hdiag_split<H, L>(e, net, sh, nxp / 16, s1, s2);
+          else
+            mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+        }
+      }
       const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
       const float c1 = 0.5f * (1.0f - e.alpha) * (float)nx / vv, c2 = 0.25f * (float)nx / vv;
       float arg[NSG], sn[NSG];
@@ -1473,7 +1643,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   bool tlast = false;
   if constexpr (TD) {
     tlast = false;  // the terminal MLP needs the noise tile before the integral rollout
-  } else if constexpr (SPLIT) {
+  } else if constexpr (SPLIT && !GBM) {
     tlast = true;  // measured faster, and the terminal sums are not live across the MLP (no spills)
   } else if constexpr (!GBM) {
     if (a.order == 1) tlast = (__builtin_amdgcn_s_getreg((3 << 11) | (16 << 6) | 4) & 1) != 0;  // HW_ID.TG_ID
@@ -1603,7 +1773,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       }
     }
   }
-  if constexpr (HESS) hess_block<KIND, H, L, ZERO>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
+  if constexpr (HESS) hess_block<KIND, H, L, ZERO, SPLIT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
 }
 
 }  // namespace dpi

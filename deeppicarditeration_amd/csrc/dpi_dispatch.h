@@ -39,7 +39,7 @@ struct Launch {
 template <int KIND, int H, int L, bool Z, bool TDV>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if constexpr (TDV) {
-    if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+    if constexpr (!Z && H % 32 == 0) {
       if (q.a->split)
         hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
                            net->d, *q.a);
@@ -57,10 +57,17 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
     if constexpr (KIND == DPI_EQ_GBM) {
       EqDev e2 = p->e;
       e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
+      if constexpr (!Z && H % 32 == 0) {
+        if (q.a->split) {
+          hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
+                             *q.a);
+          return;
+        }
+      }
       hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
                          *q.a);
     }
-  } else if constexpr (!Z && KIND != DPI_EQ_GBM && H % 32 == 0) {
+  } else if constexpr (!Z && H % 32 == 0) {
     if (q.a->split)
       hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
     else

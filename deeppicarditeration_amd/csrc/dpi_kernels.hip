@@ -1200,6 +1200,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.c3h1 = DPI_TAG_HTERM | (epoch << 8);
   a.c3h2 = DPI_TAG_HINT | (epoch << 8);
+  a.split = mlp_split() ? 1 : 0;  // fp16-split tangent sweeps (mlp_hdiag_split) unless DPI_GEMM_F32
   a.point_base = point_base;
   a.hpart = (float*)(b + base);
   hipStream_t st = (hipStream_t)stream;

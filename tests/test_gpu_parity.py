@@ -248,8 +248,9 @@ def test_hjb_ou_mlp_vs_oracle(mlp_precision):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-def test_gbm_config5_network_sdgd_vs_oracle():
-    """Config-5 network (3x64 ELU), SDGD v = 100, K = 50, against the fp64 oracle."""
+def test_gbm_config5_network_sdgd_vs_oracle(mlp_precision):
+    """Config-5 network (3x64 ELU), SDGD v = 100, K = 50, against the fp64 oracle; the tangent
+    sweep on the fp16-split MFMA (mlp_hdiag_split) and on the fp32 MFMA (mlp_hdiag)."""
     import deeppicarditeration_amd as dpi
     eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
     net = _random_mlp(eq, [64] * 3, 6)
@@ -260,6 +261,7 @@ def test_gbm_config5_network_sdgd_vs_oracle():
     oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
     ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 128, 50, 3, 2, 0, v=100)
     parts = rel_l2_parts(y.cpu().numpy(), ref)
+    print("gbm sdgd, mlp precision", mlp_precision, parts)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
@@ -359,9 +361,9 @@ def test_hessian_labels_golden_reference_parity(case):
         assert r < TOL, (name, r)
 
 
-def test_hessian_labels_config5_network_vs_oracle():
-    """Config-5 network (3 x 64 ELU), K = 10, M = 256, against the fp64 oracle; the Hessian block
-    is symmetric by construction."""
+def test_hessian_labels_config5_network_vs_oracle(mlp_precision):
+    """Config-5 network (3 x 64 ELU), K = 10, M = 256, against the fp64 oracle (fp16-split and fp32
+    tangent sweeps); the Hessian block is symmetric by construction."""
     import deeppicarditeration_amd as dpi
     eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
     net = _random_mlp(eq, [64] * 3, 12)
