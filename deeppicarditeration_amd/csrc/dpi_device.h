@@ -845,13 +845,18 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       for (int r = 0; r < 4; ++r) lam[l][T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
     }
   }
-  // lam_l elu''(a_l): the per-layer weights of the squared tangents
+  // lam_l elu''(a_l): the per-layer weights of the squared tangents; elu'(a_l) for the tangent
+  // propagation (computed once: the sweep below needs neither a_l nor any compare)
+  float dact[L > 1 ? L - 1 : 1][HT][4];
 #pragma unroll
   for (int l = 0; l < L; ++l)
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) lam[l][T][r] *= d2elu_from_a(act[l][T][r]);
+      for (int r = 0; r < 4; ++r) {
+        lam[l][T][r] *= d2elu_from_a(act[l][T][r]);
+        if (l < L - 1) dact[l][T][r] = delu_from_a(act[l][T][r]);
+      }
   // tangent sweep over the state dimensions
   float s1 = 0.f, s2 = 0.f;
   for (int d = 0; d < e.nx; ++d) {
@@ -870,7 +875,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l - 1][t][r]) * z[t][r];
+        for (int r = 0; r < 4; ++r) Bm[t][r] = dact[l - 1][t][r] * z[t][r];
       half8 bh[NU], bl[NU];
 #pragma unroll
       for (int u = 0; u < NU; ++u) split_act(Bm[2 * u], Bm[2 * u + 1], bh[u], bl[u]);
