@@ -767,19 +767,24 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int u = 0; u < NU; ++u) afrag(net.WS[l], 16 * T + jj, u, wh[l - 1][T][u], wl[l - 1][T][u]);
   // o = W_l B for the B operand (bh, bl) split per chunk, from the register-resident fragments
+  // (tile-inner order: HT independent accumulators between dependent MFMAs, no s_nop stalls)
   auto wmul = [&](int l, const half8 (&bh)[NU], const half8 (&bl)[NU], floatx4 (&o)[HT]) {
+    floatx4 am[HT], ac[HT];
 #pragma unroll
-    for (int T = 0; T < HT; ++T) {
-      floatx4 am = {0.f, 0.f, 0.f, 0.f}, ac = {0.f, 0.f, 0.f, 0.f};
+    for (int T = 0; T < HT; ++T) am[T] = ac[T] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        am = mfma16(wh[l - 1][T][u], bh[u], am);
-        ac = mfma16(wh[l - 1][T][u], bl[u], ac);
-        ac = mfma16(wl[l - 1][T][u], bh[u], ac);
-      }
+    for (int u = 0; u < NU; ++u) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
+      for (int T = 0; T < HT; ++T) am[T] = mfma16(wh[l - 1][T][u], bh[u], am[T]);
+#pragma unroll
+      for (int T = 0; T < HT; ++T) ac[T] = mfma16(wh[l - 1][T][u], bl[u], ac[T]);
+#pragma unroll
+      for (int T = 0; T < HT; ++T) ac[T] = mfma16(wl[l - 1][T][u], bh[u], ac[T]);
     }
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[T][r] = fmaf(ac[T][r], SPLIT_INV, am[T][r]);
   };
   float act[L][HT][4];
   float lam[L][HT][4];
