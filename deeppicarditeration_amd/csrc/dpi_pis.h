@@ -253,23 +253,56 @@ __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx,
   }
 }
 
+// GMM parameters staged in LDS per workgroup (the per-dimension gathers of pis_z_stats would
+// otherwise be ~1,000 vector loads per thread): gm[0] = means, gm[1] = inverse variances,
+// [component][dim], zero beyond nx.
+struct PisGmmLds {
+  float m[NSG][NXP_MAX];
+  float iv[NSG][NXP_MAX];
+};
+__device__ __forceinline__ void pis_stage_gmm(const EqDev& e, PisGmmLds& g) {
+  for (int idx = threadIdx.x; idx < NSG * NXP_MAX; idx += blockDim.x) {
+    const int c = idx / NXP_MAX, d = idx - c * NXP_MAX;
+    const bool ok = c < e.ncomp && d < e.nx;
+    g.m[c][d] = ok ? e.mean[c * e.nx + d] : 0.f;
+    g.iv[c][d] = ok ? e.ivar[c * e.nx + d] : 0.f;
+  }
+}
+
 // grad_x u for one row, reduced into the OU statistics A = sum (X - mu) z, B = sum z^2.
 // 4 threads per row (consecutive lanes, q = 0..3).  fp32 rows: dims d = q, q+4, ...; split rows:
-// the dims of granule pairs (u, q) — d = 32u + 4q + (j & 3) + 16 (j >> 2) — read 32 B at a time.
+// the dims of granule pairs (u, q) — d = 32u + 4q + (j & 3) + 16 (j >> 2) — read 32 B at a time,
+// all of this thread's row data loaded into registers in one batch before the two GMM passes.
 template <bool X3>
-__device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn, const float* row, const PisRows& L,
-                                            float lbd, int q, float& A_out, float& B_out, float& smooth_out) {
+__device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn, const PisGmmLds& g, const float* row,
+                                            const PisRows& L, float lbd, int q, float& A_out, float& B_out,
+                                            float& smooth_out) {
   const int nx = e.nx;
+  constexpr int NXC = NXP_MAX / 32;
   // smooth = smooth_net(emb(lbd))[0] - smooth_net(emb(0))[0]  (solution.py:236-254)
   float sr = 0.f;
+  float xs[NXC][8], js[NXC][8];  // X_d and (J^T X + net_out)_d of this thread's dims
+  int nxc = 0;
   if constexpr (X3) {
+    nxc = L.INP / 32 - 2;
+    float hv[PIS_CH / 32][8];
 #pragma unroll
-    for (int u = 0; u < PIS_CH / 32; ++u) {
-      float v[8];
-      x3_get8(row, L.H0, u, q, v);
+    for (int u = 0; u < PIS_CH / 32; ++u) x3_get8(row, L.H0, u, q, hv[u]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], v[j], sr);
+    for (int u = 0; u < NXC; ++u) {
+      if (u < nxc) {
+        float gv[8], nv[8];
+        x3_get8(row, L.IN, 2 + u, q, xs[u]);
+        x3_get8(row, L.GX, u, q, gv);
+        x3_get8(row, L.NO, u, q, nv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) js[u][j] = gv[j] + nv[j];
+      }
     }
+#pragma unroll
+    for (int u = 0; u < PIS_CH / 32; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], hv[u][j], sr);
   } else {
     for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
   }
@@ -280,16 +313,14 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
   // visit(d, X_d, (J^T X + net_out)_d) over this thread's dims
   auto for_dims = [&](auto&& visit) {
     if constexpr (X3) {
-      const int nxc = L.INP / 32 - 2;
-      for (int u = 0; u < nxc; ++u) {
-        float xv[8], gv[8], nv[8];
-        x3_get8(row, L.IN, 2 + u, q, xv);
-        x3_get8(row, L.GX, u, q, gv);
-        x3_get8(row, L.NO, u, q, nv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
-          if (d < nx) visit(d, xv[j], gv[j] + nv[j]);
+      for (int u = 0; u < NXC; ++u) {
+        if (u < nxc) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
+            if (d < nx) visit(d, xs[u][j], js[u][j]);
+          }
         }
       }
     } else {
@@ -306,8 +337,8 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
 #pragma unroll
     for (int c = 0; c < NSG; ++c)
       if (c < e.ncomp) {
-        const float df = y - e.mean[c * nx + d];
-        st[c] = fmaf(df * df, e.ivar[c * nx + d], st[c]);
+        const float df = y - g.m[c][d];
+        st[c] = fmaf(df * df, g.iv[c][d], st[c]);
       }
   });
   float lp[NSG], mx = -3.0e38f;
@@ -325,13 +356,15 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
     ws += w[c];
   }
   const float iws = 1.0f / ws;
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) w[c] *= iws;
   float A = 0.f, B = 0.f;
   for_dims([&](int d, float Xd, float jn) {
     const float y = decay * Xd;
     float gg = 0.f;
 #pragma unroll
     for (int c = 0; c < NSG; ++c)
-      if (c < e.ncomp) gg = fmaf(w[c] * iws, (y - e.mean[c * nx + d]) * e.ivar[c * nx + d], gg);
+      if (c < e.ncomp) gg = fmaf(w[c], (y - g.m[c][d]) * g.iv[c][d], gg);
     const float z = smooth * jn + (1.0f - smooth) * decay * gg;
     A = fmaf(Xd - e.ou_mu, z, A);
     B = fmaf(z, z, B);
@@ -347,13 +380,16 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
 
 // Baseline f_b (state part) and nothing else: one 64-thread block per 16 points.
 template <int KIND, bool X3>
-__global__ void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L, int n,
+__global__ __launch_bounds__(64) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L, int n,
                                  float* __restrict__ fb) {
+  __shared__ PisGmmLds gmm;
+  pis_stage_gmm(e, gmm);
+  __syncthreads();
   const int i = blockIdx.x * 16 + (threadIdx.x >> 2), q = threadIdx.x & 3;
   const int ic = min(i, n - 1);
   const float* row = rows + (size_t)ic * L.stride;
   float A, B, sm;
-  pis_z_stats<X3>(e, pn, row, L, pn.T - row[L.SC + 0], q, A, B, sm);
+  pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - row[L.SC + 0], q, A, B, sm);
   if (i < n && q == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, A, B);
 }
 
@@ -444,6 +480,9 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
                                                    const float* __restrict__ rows, PisRows L,
                                                    float* __restrict__ partial, float td_dt) {
   __shared__ float cs[2][P][NXP_MAX + 4];  // per-path contributions and their squares: [path][col]
+  __shared__ PisGmmLds gmm;
+  pis_stage_gmm(e, gmm);
+  __syncthreads();
   const int tid = threadIdx.x;
   const int g = g0 + blockIdx.x;
   const int i = g / nbp, b = g - i * nbp;
@@ -457,7 +496,7 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;
   const float s = row[L.SC + 0], ap = row[L.SC + 2], smt = row[L.SC + 3];
   float A, B, sm;
-  pis_z_stats<X3>(e, pn, row, L, pn.T - s, q, A, B, sm);
+  pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
   const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * smt) * e.asq);
   if (q == 0) {
