@@ -24,25 +24,35 @@ for wl in ("burgers", "hjb", "gbm", "gbm_hess"):
     b = src / f"bench_{wl}.log"
     if b.exists():
         shutil.copy(b, dst / f"{tag}_bench_{wl}_n1.log")
-pmc = {}
-for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    f = src / f"pmc_{c}" / "pmc_counter_collection.csv"
-    if not f.exists():
+# HBM traffic per label_moments call, per workload: separate --pmc passes (FETCH_SIZE, WRITE_SIZE) over
+# the bench; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction.  A call is one launch
+# of the anchor kernel (k_paths, or k_pis_rollout for the PISGradNet chain); the bytes of every
+# kernel of the call (rollout, GEMM chain, final, reduce) are summed.
+ANCHOR = {"burgers": "dpi::k_paths", "gbm": "dpi::k_paths", "gbm_hess": "dpi::k_paths", "hjb": "dpi::k_pis_rollout"}
+for wl, anchor in ANCHOR.items():
+    pmc = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        f = src / f"pmc_{wl}_{c}" / "pmc_counter_collection.csv"
+        if not f.exists():
+            continue
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            agg[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(r["Counter_Value"]))
+        pmc[c] = {k: {"dispatches": len(v), "total_kb": sum(v)} for k, v in agg.items()}
+        (dst / f"{tag}_pmc_{wl}_{c}.json").write_text(json.dumps(
+            {"command": f"rocprofv3 --pmc {c} --kernel-include-regex 'k_paths|k_pis|k_gemm|k_reduce' -- python "
+                        f"bench.py --workload {wl} --steps 10 --warmup 2 --no-cpu-baseline", "kernels": pmc[c]},
+            indent=1))
+    if len(pmc) < 2:
         continue
-    agg = collections.defaultdict(list)
-    for r in csv.DictReader(open(f)):
-        agg[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(r["Counter_Value"]))
-    pmc[c] = {k: {"dispatches": len(v), "avg_kb_per_dispatch": sum(v) / len(v)} for k, v in agg.items()}
-    (dst / f"{tag}_pmc_{c}.json").write_text(json.dumps(
-        {"command": f"rocprofv3 --pmc {c} --kernel-include-regex 'k_paths|k_pis|k_gemm' -- python bench.py "
-                    "--steps 10 --warmup 2 --no-cpu-baseline", "kernels": pmc[c]}, indent=1))
-if pmc:
-    k = next(k for k in pmc["FETCH_SIZE"] if k.startswith("dpi::k_paths"))
-    fe, wr = pmc["FETCH_SIZE"][k]["avg_kb_per_dispatch"], pmc["WRITE_SIZE"][k]["avg_kb_per_dispatch"]
-    t = {"kernel": k, "workload": "Burgers cfg2 16 x 4096 K=50 (bench.py default)", "FETCH_SIZE_KB": fe,
-         "WRITE_SIZE_KB": wr, "hbm_bytes_per_launch": (2 * fe + wr) * 1024,
+    calls = sum(v["dispatches"] for k, v in pmc["FETCH_SIZE"].items() if k.startswith(anchor))
+    fe = sum(v["total_kb"] for v in pmc["FETCH_SIZE"].values()) / calls
+    wr = sum(v["total_kb"] for v in pmc["WRITE_SIZE"].values()) / calls
+    t = {"workload": wl, "anchor_kernel": anchor, "calls": calls, "FETCH_SIZE_KB_per_call": fe,
+         "WRITE_SIZE_KB_per_call": wr, "hbm_bytes_per_launch": (2 * fe + wr) * 1024,
          "note": "separate --pmc passes; FETCH_SIZE doubled per the gfx950 correction (an upper bound for the "
-                 "non-16-B loads); Infinity-Cache hits are counted by these fabric-side counters",
-         "source": f"profiles/{tag}_pmc_FETCH_SIZE.json, profiles/{tag}_pmc_WRITE_SIZE.json"}
-    (dst / "traffic_burgers.json").write_text(json.dumps(t, indent=1))
+                 "non-16-B loads); Infinity-Cache hits are counted by these fabric-side counters; all kernels of "
+                 "one label_moments call summed",
+         "source": f"profiles/{tag}_pmc_{wl}_FETCH_SIZE.json, profiles/{tag}_pmc_{wl}_WRITE_SIZE.json"}
+    (dst / f"traffic_{wl}.json").write_text(json.dumps(t, indent=1))
     print(json.dumps(t, indent=1))

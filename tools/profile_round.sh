@@ -15,7 +15,9 @@ for wl in burgers gbm gbm_hess hjb; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_$wl -o trace --output-format csv -- \
     python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_$wl.log 2>&1
 done
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm" -d $out/pmc_$c -o pmc --output-format csv -- \
-    python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_$c.log 2>&1
+for wl in burgers hjb gbm gbm_hess; do
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm|k_reduce" -d $out/pmc_${wl}_$c -o pmc \
+      --output-format csv -- python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_${wl}_$c.log 2>&1
+  done
 done
