@@ -290,16 +290,18 @@ def test_hjb_pisgradnet_config3_network_vs_oracle(gemm_mode):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-def test_full_size_determinism_and_shard_invariance():
+@pytest.mark.parametrize("delta_t", [0.0, 0.3])
+def test_full_size_determinism_and_shard_invariance(delta_t):
     """BASELINE config 2 size (16 x 4096 paths, K = 50): bitwise-reproducible labels, and moments
-    computed as two MC shards + dpi_moments_reduce equal the single call bit for bit."""
+    computed as two MC shards + dpi_moments_reduce equal the single call bit for bit; also with the
+    TD estimators (delta_t = 0.3)."""
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd import _lib as L
     eq = dpi.Cha(100, 1.0, 5.0, 1.0)
     net = _random_mlp(eq, [128] * 4, 5)
     M = 4096
     gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
-                                  n_estimate_integral=M, n_euler_steps=50, seed=1)
+                                  n_estimate_integral=M, n_euler_steps=50, seed=1, estimate_delta_t=delta_t)
     tx, _ = gen.sample_t_and_x(16, point_base=0)
     ws = gen.point_baseline(tx)
     full = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
