@@ -67,6 +67,10 @@ struct NetDev {
   const uint32_t* W1xTS;     // (nxp32, H)
   const uint32_t* WS[4];     // (H, H)
   const uint32_t* WTS[4];
+  // hidden layers for the split tangent sweep (mlp_hdiag_split): lo unscaled, prescaled by
+  // 2^s (max |2^s W| in [0.5, 1)), wus = 2^-s (pack_split_x3)
+  const uint32_t* WU[4];     // (H, H)
+  float wus[4];
 };
 
 // ------------------------------------------------------------------------------ helpers
@@ -736,19 +740,32 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 }
 
 // mlp_hdiag on the fp16-split MFMA (H % 32 == 0): same inputs and outputs.  The hidden layers'
-// split weights (NetDev::WS, fragment order) are loaded ONCE into registers as MFMA A fragments
-// (2 (L - 1) (H / 16) (H / 32) half8 pairs: 128 VGPRs at H = 64, L = 3) and reused by the forward
-// pass and by every direction of the tangent sweep, which then runs without LDS traffic: per
-// direction and layer (H/16)(H/32) x 3 v_mfma_f32_16x16x32_f16 instead of (H/16)(H/4)
-// v_mfma_f32_16x16x4_f32 (5.3x fewer MFMA cycles); the tangent / activation B operands are split
-// in registers.  Layer 0 (the noise tile through W1x) and the z_0 = W1x[:, d] lookups stay fp32
-// from LDS; the adjoint reads the transposed split weights (WTS) from L2 once.
+// split weights (NetDev::WU: lo unscaled, matrix prescaled by 2^s) are loaded ONCE into registers
+// as MFMA A fragments (2 (L - 1) (H / 16) (H / 32) half8: 128 VGPRs at H = 64, L = 3) and reused by
+// the forward pass and by every direction of the tangent sweep, which then runs without LDS
+// traffic: per direction and layer (H/16)(H/32) x 3 v_mfma_f32_16x16x32_f16 (hi hi + hi lo + lo hi
+// into one accumulator) instead of (H/16)(H/4) v_mfma_f32_16x16x4_f32.  B operands are split in
+// registers with the same unscaled-lo convention, prescaled by a power of two so their residuals
+// stay fp16-normal; every scale is a power of two folded into per-unit constants computed once
+// (ELU' x scale for the next layer's operand, lam elu'' / scale^2 for the squared tangents), so a
+// direction costs per element one multiply, the split and one FMA.  Layer 0 (the noise tile
+// through W1x) and z_0 = W1x[:, d] stay fp32 from LDS; the adjoint reads the transposed split
+// weights (WTS) from L2 once.
+__device__ __forceinline__ void split8u(const float (&x)[8], half8& hi, half8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)x[j];
+    hi[j] = h;
+    lo[j] = (_Float16)(x[j] - (float)h);
+  }
+}
 template <int H, int L>
 __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
                                                 float& s1_out, float& s2_out) {
   static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
   constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
   constexpr int WXS = LdsGbm<H>::WXS;
+  constexpr float SA = 16.0f, SB = 64.0f;  // operand prescales: activations, tangents
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int jj = lane & 15, qq = lane >> 4;
   const int pp = 16 * wv + jj;
@@ -765,26 +782,33 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
-      for (int u = 0; u < NU; ++u) afrag(net.WS[l], 16 * T + jj, u, wh[l - 1][T][u], wl[l - 1][T][u]);
-  // o = W_l B for the B operand (bh, bl) split per chunk, from the register-resident fragments
-  // (tile-inner order: HT independent accumulators between dependent MFMAs, no s_nop stalls)
-  auto wmul = [&](int l, const half8 (&bh)[NU], const half8 (&bl)[NU], floatx4 (&o)[HT]) {
-    floatx4 am[HT], ac[HT];
+      for (int u = 0; u < NU; ++u) afrag(net.WU[l], 16 * T + jj, u, wh[l - 1][T][u], wl[l - 1][T][u]);
+  // B operand (C layout, HT tiles x 4) x scale -> split halves per 32-wide chunk
+  auto split_b = [&](const float (&x)[HT][4], const float (&f)[HT][4], half8 (&bh)[NU], half8 (&bl)[NU]) {
 #pragma unroll
-    for (int T = 0; T < HT; ++T) am[T] = ac[T] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NU; ++u) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = f[2 * u][r] * x[2 * u][r];
+        v[4 + r] = f[2 * u + 1][r] * x[2 * u + 1][r];
+      }
+      split8u(v, bh[u], bl[u]);
+    }
+  };
+  // o = W'_l B (one accumulator per tile; tile-inner order between dependent products)
+  auto wmul = [&](int l, const half8 (&bh)[NU], const half8 (&bl)[NU], floatx4 (&o)[HT]) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T) o[T] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
 #pragma unroll
-      for (int T = 0; T < HT; ++T) am[T] = mfma16(wh[l - 1][T][u], bh[u], am[T]);
+      for (int T = 0; T < HT; ++T) o[T] = mfma16(wh[l - 1][T][u], bh[u], o[T]);
 #pragma unroll
-      for (int T = 0; T < HT; ++T) ac[T] = mfma16(wh[l - 1][T][u], bl[u], ac[T]);
+      for (int T = 0; T < HT; ++T) o[T] = mfma16(wh[l - 1][T][u], bl[u], o[T]);
 #pragma unroll
-      for (int T = 0; T < HT; ++T) ac[T] = mfma16(wl[l - 1][T][u], bh[u], ac[T]);
+      for (int T = 0; T < HT; ++T) o[T] = mfma16(wl[l - 1][T][u], bh[u], o[T]);
     }
-#pragma unroll
-    for (int T = 0; T < HT; ++T)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[T][r] = fmaf(ac[T][r], SPLIT_INV, am[T][r]);
   };
   float act[L][HT][4];
   float lam[L][HT][4];
@@ -807,20 +831,27 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
     }
   }
-  // hidden layers (split MFMA)
-#pragma unroll
-  for (int l = 1; l < L; ++l) {
-    half8 bh[NU], bl[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) split_act(act[l - 1][2 * u], act[l - 1][2 * u + 1], bh[u], bl[u]);
-    floatx4 o[HT];
-    wmul(l, bh, bl, o);
+  // hidden layers: B = SA a_{l-1}, o = 2^s SA W a -> a_l = elu(o wus / SA + b)
+  {
+    float ones[HT][4];
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(o[T][r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+      for (int r = 0; r < 4; ++r) ones[T][r] = SA;
+#pragma unroll
+    for (int l = 1; l < L; ++l) {
+      half8 bh[NU], bl[NU];
+      split_b(act[l - 1], ones, bh, bl);
+      floatx4 o[HT];
+      wmul(l, bh, bl, o);
+      const float sc = net.wus[l] * (1.0f / SA);
+#pragma unroll
+      for (int T = 0; T < HT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) act[l][T][r] = elu(fmaf(o[T][r], sc, sh.bh[l * H + 16 * T + 4 * qq + r]));
+    }
   }
-  // adjoints lam_l = du/da_l: lam_l = W_{l+1}^T (elu'(a_{l+1}) lam_{l+1})
+  // adjoints lam_l = du/da_l: lam_l = W_{l+1}^T (elu'(a_{l+1}) lam_{l+1})  (scaled-lo WTS, once per path)
 #pragma unroll
   for (int T = 0; T < HT; ++T)
 #pragma unroll
@@ -850,18 +881,22 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       for (int r = 0; r < 4; ++r) lam[l][T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
     }
   }
-  // lam_l elu''(a_l): the per-layer weights of the squared tangents; elu'(a_l) for the tangent
-  // propagation (computed once: the sweep below needs neither a_l nor any compare)
-  float dact[L > 1 ? L - 1 : 1][HT][4];
+  // per-unit constants of the sweep.  Tangent of layer l >= 1 is held as z'_l = (SB / wus_l) z_l
+  // (the raw accumulator); the next operand is SB elu'(a_l) z_l = (elu'(a_l) wus_l) z'_l, and
+  // lam_l elu''(a_l) z_l^2 = (lam_l elu''(a_l) (wus_l / SB)^2) z'_l^2.
+  float fz[L > 1 ? L - 1 : 1][HT][4];
 #pragma unroll
-  for (int l = 0; l < L; ++l)
+  for (int l = 0; l < L; ++l) {
+    const float zs = l == 0 ? 1.0f : net.wus[l] * (1.0f / SB);
+    const float bs = l == 0 ? SB : net.wus[l];
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        lam[l][T][r] *= d2elu_from_a(act[l][T][r]);
-        if (l < L - 1) dact[l][T][r] = delu_from_a(act[l][T][r]);
+        lam[l][T][r] *= d2elu_from_a(act[l][T][r]) * (zs * zs);
+        if (l < L - 1) fz[l][T][r] = delu_from_a(act[l][T][r]) * bs;
       }
+  }
   // tangent sweep over the state dimensions
   float s1 = 0.f, s2 = 0.f;
   for (int d = 0; d < e.nx; ++d) {
@@ -872,18 +907,12 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
-        term = fmaf(lam[0][T][r], z[T][r] * z[T][r], term);
+        term = fmaf(lam[0][T][r] * z[T][r], z[T][r], term);
       }
 #pragma unroll
     for (int l = 1; l < L; ++l) {
-      float Bm[HT][4];
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Bm[t][r] = dact[l - 1][t][r] * z[t][r];
       half8 bh[NU], bl[NU];
-#pragma unroll
-      for (int u = 0; u < NU; ++u) split_act(Bm[2 * u], Bm[2 * u + 1], bh[u], bl[u]);
+      split_b(z, fz[l - 1], bh, bl);
       floatx4 o[HT];
       wmul(l, bh, bl, o);
 #pragma unroll
@@ -891,7 +920,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           z[T][r] = o[T][r];
-          term = fmaf(lam[l][T][r], o[T][r] * o[T][r], term);
+          term = fmaf(lam[l][T][r] * o[T][r], o[T][r], term);
         }
     }
     const float ud = qsum(term);

@@ -376,7 +376,8 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   const float bout = cur[H];
   // fp16-split copies for the split MFMA path (H % 32 == 0)
   const int nxp32 = (nx + 31) & ~31;
-  size_t oW1xS = 0, oW1xTS = 0, oWS[4] = {0}, oWTS[4] = {0};
+  size_t oW1xS = 0, oW1xTS = 0, oWS[4] = {0}, oWTS[4] = {0}, oWU[4] = {0};
+  float wus[4] = {1.f, 1.f, 1.f, 1.f};
   if (H % 32 == 0) {
     auto Wx = [&](int h, int d) { return d < nx ? W0[(size_t)h * n_in + 1 + d] : 0.f; };
     oW1xS = pack_split(blob, H, nxp32, Wx);
@@ -386,6 +387,7 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
       std::vector<float> Wc(Wl, Wl + (size_t)H * H);
       oWS[l] = pack_split(blob, H, H, [&](int r, int c) { return Wc[(size_t)r * H + c]; });
       oWTS[l] = pack_split(blob, H, H, [&](int r, int c) { return Wc[(size_t)c * H + r]; });
+      oWU[l] = pack_split_x3(blob, H, H, [&](int r, int c) { return Wc[(size_t)r * H + c]; }, &wus[l]);
     }
   }
   auto* n = new dpi_net_s();
@@ -427,6 +429,8 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
     for (int l = 1; l < L; ++l) {
       n->d.WS[l] = u32(oWS[l]);
       n->d.WTS[l] = u32(oWTS[l]);
+      n->d.WU[l] = u32(oWU[l]);
+      n->d.wus[l] = wus[l];
     }
   }
   *out = n;
