@@ -322,6 +322,35 @@ def test_full_size_determinism_and_shard_invariance(delta_t):
     torch.testing.assert_close(yT + yI, y, rtol=1e-5, atol=1e-5)
 
 
+def test_config4_burgers_2M_paths_sharded_8_ways():
+    """BASELINE configs[3] shape: Burgers, 512 points x 4096 MC paths (2,097,152 path-labels),
+    K = 50, MC-sharded 8 ways (512 paths per shard, as on 8 GPUs): the 8 shard moments reduced
+    with dpi_moments_reduce equal the single call bit for bit, and two of the points (first and
+    last) match the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    net = _random_mlp(eq, [128] * 4, 0)
+    n, M, G, K = 512, 4096, 8, 50
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    ws = gen.point_baseline(tx)
+    full = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+    parts = torch.stack([gen.label_moments(tx, 0, M, r * M // G, (r + 1) * M // G, L.DPI_BOTH, ws)
+                         for r in range(G)]).contiguous()
+    red = gen.moments_reduce(parts)
+    assert torch.equal(red, full)
+    y = gen.finalize(full, M, L.DPI_BOTH, ws).cpu().numpy()
+    assert np.isfinite(y).all()
+    oeq, onet = O.Cha(100, 1.0, 5.0, 1.0), _oracle_mlp(net)
+    txh = tx.cpu().double().numpy()
+    for i in (0, n - 1):
+        ref = O.labels_grad(oeq, onet, txh[i:i + 1], M, K, 1, 1, i)
+        parts_i = rel_l2_parts(y[i:i + 1], ref)
+        assert parts_i["value"] < TOL and parts_i["grad"] < TOL, (i, parts_i)
+
+
 def test_unsupported_configurations_fail_loudly():
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd._lib import DPIError
