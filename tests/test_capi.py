@@ -52,6 +52,12 @@ def test_host_side_argument_errors_without_gpu():
     rc = lib.dpi_label_moments(h, n, ctypes.c_void_p(16), 4, 4096, 50, 1, 0, 0, 0, 100, 3, ctypes.c_void_p(16),
                                ctypes.c_void_p(16), 1 << 30, None)
     assert rc == _lib.DPI_ERR_ARG and "multiple of 64" in _lib.last_error()
+    # estimator / precision settings validate their arguments
+    assert lib.dpi_problem_set_estimate_delta_t(h, -0.1) == _lib.DPI_ERR_ARG
+    assert lib.dpi_problem_set_estimate_delta_t(h, float("nan")) == _lib.DPI_ERR_ARG
+    assert lib.dpi_problem_set_estimate_delta_t(h, 0.25) == 0 and lib.dpi_problem_set_estimate_delta_t(h, 0.0) == 0
+    assert lib.dpi_problem_set_hessian_approximation(h, 256) == _lib.DPI_ERR_ARG
+    assert lib.dpi_set_gemm_precision(7) == _lib.DPI_ERR_ARG
     assert lib.dpi_net_destroy(n) == 0 and lib.dpi_problem_destroy(h) == 0
 
 
