@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed steps for this long before the warmup")
     ap.add_argument("--cpu-sample-paths", type=int, default=512, help="MC paths per point in the CPU sample")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="burgers")
+    ap.add_argument("--pipelined", action="store_true", help="two-phase labels also at N = 1 (default: N > 1 only)")
     return ap.parse_args()
 
 
@@ -160,15 +161,31 @@ def main():
     # path-kernel timing with events on the stream the kernels run on (torch's current stream)
     ev = []
 
+    # N > 1: two-phase labels, so step i's RCCL all-gather (on RCCL's stream) overlaps step i+1's
+    # kernels; every step's full work (sampling, moments, gather, reduce, finalize) still runs
+    # inside the timed region (the pipeline is drained before it starts and at its end).
+    pipelined = (world > 1 or args.pipelined) and not wl.get("hess")
+    pending = []
+
     def step():
         tx, pb = gen.sample_t_and_x(N_POINTS)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if wl.get("hess"):
             y = labeler.labels_hessians(tx, pb, on_moments_begin=lambda: e0.record(),
                                         on_moments_end=lambda: e1.record())
+        elif pipelined:
+            pending.append(labeler.begin(tx, pb, on_moments_begin=lambda: e0.record(),
+                                         on_moments_end=lambda: e1.record()))
+            y = labeler.end(pending.pop(0)) if len(pending) > 1 else None
         else:
             y = labeler.labels(tx, pb, on_moments_begin=lambda: e0.record(), on_moments_end=lambda: e1.record())
         ev.append((e0, e1))
+        return y
+
+    def drain():
+        y = None
+        while pending:
+            y = labeler.end(pending.pop(0))
         return y
 
     # Clock ramp: the GPU needs ~10 ms of load to leave its idle clocks, which a 20-step run at
@@ -189,6 +206,7 @@ def main():
             break
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     ev.clear()
     if dist:
@@ -197,6 +215,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         y = step()
+    y = drain() if pipelined else y
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -178,10 +178,20 @@ class OnlineDataGenerator:
         return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
-    def point_baseline(self, tx, hessians=False):
+    def workspace_bytes(self, n, M, hessians=False):
+        need = self.lib.dpi_workspace_bytes(self.problem, self.net.handle, n, M)
+        if hessians:
+            need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
+        return need
+
+    def point_baseline(self, tx, hessians=False, ws=None):
+        """Per-point baseline into the generator's workspace, or into `ws` (uint8, >= workspace_bytes)."""
         n = tx.shape[0]
         M = max(self.n_estimate_terminal, self.n_estimate_integral)
-        ws = self._workspace(n, M, hessians)
+        if ws is None:
+            ws = self._workspace(n, M, hessians)
+        elif ws.numel() < self.workspace_bytes(n, M, hessians):
+            raise ValueError("workspace too small")
         _lib.check(self.lib.dpi_point_baseline(self.problem, self.net.handle, _ptr(tx), n, _ptr(ws), ws.numel(),
                                                _stream(self.device)), "dpi_point_baseline")
         return ws

@@ -61,6 +61,48 @@ class ShardedLabeler:
             on_moments_end()
         return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
 
+    # ------------------------------------------------------------------ two-phase (pipelined) labels
+    def begin(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
+        """First half of labels(): this rank's moments and, for world > 1, an asynchronous
+        all-gather of them (RCCL runs on its own stream, so the caller can enqueue the next batch's
+        kernels while it is in flight).  Two workspaces alternate, so one batch may be pending
+        while the next begins.  Returns the handle end() turns into labels."""
+        from . import _lib
+        flags = _lib.DPI_BOTH if flags is None else flags
+        M = self.gen.n_estimate_integral
+        if self.gen.n_estimate_terminal != M:
+            raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
+        n = tx.shape[0]
+        need = self.gen.workspace_bytes(n, M)
+        if not hasattr(self, "_ws_pool") or self._ws_pool[0].numel() < need:
+            dev = getattr(tx, "device", "cpu")
+            self._ws_pool = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._ws_next = 0
+        ws = self._ws_pool[self._ws_next]
+        self._ws_next ^= 1
+        self.gen.point_baseline(tx, ws=ws)
+        m0, m1 = self.shard(M)
+        if on_moments_begin:
+            on_moments_begin()
+        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags, ws)
+        if on_moments_end:
+            on_moments_end()
+        if self.world == 1:
+            return (ws, mom, None, None, flags, M)
+        import torch.distributed as dist
+        mom = mom.contiguous()
+        flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
+        work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
+        return (ws, flat, work, tuple(mom.shape), flags, M)
+
+    def end(self, pending):
+        """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
+        ws, mom, work, shape, flags, M = pending
+        if work is not None:
+            work.wait()  # the current stream waits for RCCL's, not the host
+            mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
+        return self.gen.finalize(mom, M, flags, ws)
+
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""
         from . import _lib

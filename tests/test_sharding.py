@@ -34,8 +34,11 @@ class OracleGen:
         self.n_estimate_terminal = self.n_estimate_integral = M
         self.gx = None
 
-    def point_baseline(self, tx):
-        return tx
+    def point_baseline(self, tx, ws=None):
+        return tx if ws is None else ws
+
+    def workspace_bytes(self, n, M_):
+        return 8
 
     def label_moments(self, tx, point_base, M_, m0, m1, flags, ws):
         out = np.zeros((tx.shape[0], 2, NX + 1), np.float32)
@@ -60,6 +63,20 @@ class OracleGen:
         return torch.from_numpy(y)
 
 
+class OracleGenTwoPhase(OracleGen):
+    """For begin()/end(): g(x) per batch is recomputed at finalize (the device path keeps it in the
+    batch's own workspace)."""
+
+    def finalize(self, mom, M_, flags, ws):
+        y = mom[:, 0].numpy() / M_
+        y[:, 0] += self.eq.g(self._tx[:, 1:])[:, 0]
+        return torch.from_numpy(y)
+
+    def label_moments(self, tx, point_base, M_, m0, m1, flags, ws):
+        self._tx = np.asarray(tx)
+        return super().label_moments(tx, point_base, M_, m0, m1, flags, ws)
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -69,6 +86,42 @@ def _worker(rank, world, port, q):
     y = lab.labels(tx, 0)
     q.put((rank, y.numpy()))
     dist.destroy_process_group()
+
+
+def _worker_two_phase(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    lab = ShardedLabeler(OracleGenTwoPhase(eq, net), rank=rank, world=world)
+    # the bench's pipeline: batch b + 1 begins (moments, async all-gather) before batch b ends
+    pa = lab.begin(tx, 0)
+    pb = lab.begin(tx, 100)
+    ya = lab.end(pa)
+    yb = lab.end(pb)
+    q.put((rank, ya.numpy(), yb.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_two_phase_pipeline_equals_labels():
+    """ShardedLabeler.begin/end (async all-gather, two batches in flight) give the same labels,
+    bit for bit, as the single-rank labels() of each batch."""
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    single_a = ShardedLabeler(OracleGen(eq, net), 0, 1).labels(tx, 0).numpy()
+    single_b = ShardedLabeler(OracleGen(eq, net), 0, 1).labels(tx, 100).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_two_phase, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (a, b) for r, a, b in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert res[r][0].tobytes() == single_a.tobytes()
+        assert res[r][1].tobytes() == single_b.tobytes()
 
 
 def test_shard_ranges():
