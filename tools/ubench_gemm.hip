@@ -419,6 +419,60 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
     return;
   }
   const uint64_t e0 = stamp();
+  if constexpr (VAR & 256) {  // epilogue stores only: raw accumulator bits, no VALU
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = m0 + wm * 64 + 16 * b + il;
+#pragma unroll
+      for (int c = 0; c < NT / 2; ++c) {
+        const int U = (n0 >> 5) + wn * (NT / 2) + c;
+        u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(OUT + (size_t)m * ldc) + 32 * U + 8 * ql);
+        g[0] = __builtin_bit_cast(u32x4_t, acc[2 * c][b]);
+        g[1] = __builtin_bit_cast(u32x4_t, acc[2 * c + 1][b]);
+      }
+    }
+    return;
+  }
+  if constexpr (VAR & 512) {  // epilogue VALU only: full math, one store per thread
+    float sink = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int c = 0; c < NT / 2; ++c) {
+        const int U = (n0 >> 5) + wn * (NT / 2) + c;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * c][b][r] * wscale;
+          v[4 + r] = acc[2 * c + 1][b][r] * wscale;
+        }
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 16 + 4 * ql);
+        v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+        v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+        u32x4_t h, l;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          uint32_t hw = 0, lw = 0;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const float x = v[2 * p + e];
+            const _Float16 hi = (_Float16)x;
+            const _Float16 lo = (_Float16)(x - (float)hi);
+            hw |= (uint32_t)__builtin_bit_cast(uint16_t, hi) << (16 * e);
+            lw |= (uint32_t)__builtin_bit_cast(uint16_t, lo) << (16 * e);
+          }
+          h[p] = hw;
+          l[p] = lw;
+        }
+        sink += __uint_as_float(h[0] ^ h[1] ^ h[2] ^ h[3] ^ l[0] ^ l[1] ^ l[2] ^ l[3]);
+      }
+    }
+    OUT[(size_t)(m0 + tid % BM) * ldc + (n0 >> 5) * 32 + (tid / BM)] = sink;
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int m = m0 + wm * 64 + 16 * b + il;
@@ -576,8 +630,8 @@ void report(const char* name, int M, int Kp, int Np, const uint32_t* W, const fl
               tf, maxrel);
 }
 
-int main() {
-  const int M = 32768, Kp = 512, Np = 512;
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? std::atoi(argv[1]) : 32768, Kp = 512, Np = 512;
   uint32_t* W;
   float *X, *OUT, *REF, *AUX, *bias;
   CK(hipMalloc(&W, (size_t)Np * Kp * 4));
@@ -604,7 +658,8 @@ int main() {
   CK(hipDeviceSynchronize());
   // reference outputs: the product kernel (dpi_gemm.h, unscaled-lo split, weights prescaled 2^4)
   const int nnt = Np / 128, nmt = M / X3_BM;
-  auto prod = [&](int epi, int iters) {
+  auto prod = [&](int epi, int iters, float* dst = nullptr) {
+    if (!dst) dst = REF;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -612,10 +667,10 @@ int main() {
     for (int i = 0; i < iters; ++i) {
       if (epi == 1)
         hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
-                           1.0f / 16.0f, XU, Kp, REF, Np, bias, AUXU, Np);
+                           1.0f / 16.0f, XU, Kp, dst, Np, bias, AUXU, Np);
       else
         hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
-                           1.0f / 16.0f, XU, Kp, REF, Np, nullptr, AUXU, Np);
+                           1.0f / 16.0f, XU, Kp, dst, Np, nullptr, AUXU, Np);
     }
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
@@ -633,9 +688,17 @@ int main() {
       report<EPI_BIAS_ELU, 4, 1>("elu  v1 (old loop, no epilogue)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
       report_u<EPI_BIAS_ELU, 128>("elu  W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
       report_u<EPI_BIAS_ELU, 129>("elu  W3 no epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
+      report_u<EPI_BIAS_ELU, 128 + 256>("elu  W3 epilogue = stores only", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
+                                        bias, AUXU);
+      report_u<EPI_BIAS_ELU, 128 + 512>("elu  W3 epilogue = VALU only", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
+                                        bias, AUXU);
     } else {
       report_u<EPI_DELU, 128>("delu W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, nullptr, AUXU);
     }
+    const float us2 = prod(epi, 50);
+    std::printf("%s product k_gemm_x3 (again)       %8.2f us\n", epi == 1 ? "elu " : "delu", us2);
+    const float us3 = prod(epi, 50, OUT);
+    std::printf("%s product k_gemm_x3 (-> OUT)      %8.2f us\n", epi == 1 ? "elu " : "delu", us3);
   }
   std::printf("done\n");
   return 0;
