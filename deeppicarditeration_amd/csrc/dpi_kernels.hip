@@ -882,7 +882,7 @@ extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) 
 
 extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
                       float* tx, void* stream) {
-  if (!p || !tx || n < 0 || epoch > 0xFFFFFFu) return fail(DPI_ERR_ARG, "sample_points: bad arguments");
+  if (!p || (!tx && n) || n < 0 || epoch > 0xFFFFFFu) return fail(DPI_ERR_ARG, "sample_points: bad arguments");
   if (n == 0) return 0;
   const int nb = (p->e.nx + 3) >> 2;
   const int total = n * nb;
@@ -1020,7 +1020,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
 int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes, void* stream) {
   int rc = check_pair(p, net);
   if (rc) return rc;
-  if (!tx || !ws || n < 0) return fail(DPI_ERR_ARG, "point_baseline: bad arguments");
+  if (n < 0 || (n && (!tx || !ws))) return fail(DPI_ERR_ARG, "point_baseline: bad arguments");
   if (n == 0) return 0;
   const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
   if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
@@ -1044,7 +1044,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
                         void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
   int rc = check_pair(p, net);
   if (rc) return rc;
-  if (!tx || !ws || !moments || n < 0 || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
+  if (n < 0 || (n && (!tx || !ws || !moments)) || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
       (m_begin % P) || (m_end % P) || !(flags & DPI_BOTH) || (flags & ~DPI_BOTH) || epoch > 0xFFFFFFu)
     return fail(DPI_ERR_ARG, "label_moments: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
   if (n == 0) return 0;
@@ -1102,7 +1102,7 @@ int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M,
 }
 
 int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, void* stream) {
-  if (!parts || !out || n_parts < 1 || n < 0 || nx < 1) return fail(DPI_ERR_ARG, "moments_reduce: bad arguments");
+  if (n < 0 || (n && (!parts || !out)) || n_parts < 1 || nx < 1) return fail(DPI_ERR_ARG, "moments_reduce: bad arguments");
   if (n == 0) return 0;
   if (n_parts > 1024) return fail(DPI_ERR_ARG, "moments_reduce: at most 1024 parts");
   const int len = n * 2 * (1 + nx);
@@ -1124,7 +1124,7 @@ int dpi_sums_reduce(const float* parts, int n_parts, size_t len, float* out, voi
 
 int dpi_label_finalize(dpi_problem p, const float* moments, int n, int M, int flags, float sample_bound, float* y,
                        const void* ws, size_t ws_bytes, void* stream) {
-  if (!p || !moments || !y || !ws || n < 0 || M < 1 || ws_bytes < (size_t)n * 4)
+  if (!p || n < 0 || (n && (!moments || !y || !ws)) || M < 1 || ws_bytes < (size_t)n * 4)
     return fail(DPI_ERR_ARG, "label_finalize: bad arguments");
   if (n == 0) return 0;
   const int F = 1 + p->e.nx;
@@ -1139,6 +1139,7 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
                                 float* moments, void* ws, size_t ws_bytes, void* stream) {
   int rc = check_pair(p, net);
   if (rc) return rc;
+  if (n < 0 || M < 1 || K < 1) return fail(DPI_ERR_ARG, "generate_with_gradients: bad arguments (n >= 0, M, K >= 1)");
   if (n == 0) return 0;
   const int F = 1 + p->e.nx;
   const WsLayout w = ws_layout(net, n, M, F);
@@ -1172,7 +1173,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   if (p->e.kind != DPI_EQ_GBM)
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
   if (net->d.kind == 2) return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: MLP or ZeroSolution networks only");
-  if (!tx || !ws || !moments || n < 0 || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
+  if (n < 0 || (n && (!tx || !ws || !moments)) || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
       (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu)
     return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
   if (n == 0) return 0;
@@ -1231,7 +1232,7 @@ int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int 
 
 int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M,
                                 float sample_bound, float* y, void* ws, size_t ws_bytes, void* stream) {
-  if (!p || !moments || !hessian_sums || !y || !ws || n < 0 || M < 1)
+  if (!p || n < 0 || (n && (!moments || !hessian_sums || !y || !ws)) || M < 1)
     return fail(DPI_ERR_ARG, "label_finalize_hessians: bad arguments");
   if (n == 0) return 0;
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx;
@@ -1252,7 +1253,7 @@ int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const f
                                              float* y, void* ws, size_t ws_bytes, void* stream) {
   int rc = check_pair(p, net);
   if (rc) return rc;
-  if (!y || M < P || (M % P) || M > 1024 * P)
+  if (n < 0 || (!y && n) || M < P || (M % P) || M > 1024 * P)
     return fail(DPI_ERR_ARG, "generate_with_gradients_and_hessians: bad arguments (M multiple of 64, <= 65536)");
   if (n == 0) return 0;
   if (p->e.kind != DPI_EQ_GBM)

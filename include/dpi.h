@@ -6,7 +6,8 @@
  * stream-ordered on `stream` (a hipStream_t; NULL = default stream) and never synchronise
  * the device, so they can be captured into a hipGraph.  Return 0 on success or a negative
  * DPI_ERR_* code; dpi_last_error() returns the thread-local message.  No C++ exception
- * crosses the ABI.
+ * crosses the ABI.  n = 0 points is a valid empty batch: the call checks its scalar arguments,
+ * launches nothing and accepts NULL data pointers.
  *
  * Reference interfaces each entry point replaces (paths relative to the reference repo):
  *   dpi_problem_create_cha   picard/equations.py:266-338  Cha(nx, alpha, k, T)

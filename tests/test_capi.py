@@ -52,6 +52,14 @@ def test_host_side_argument_errors_without_gpu():
     rc = lib.dpi_label_moments(h, n, ctypes.c_void_p(16), 4, 4096, 50, 1, 0, 0, 0, 100, 3, ctypes.c_void_p(16),
                                ctypes.c_void_p(16), 1 << 30, None)
     assert rc == _lib.DPI_ERR_ARG and "multiple of 64" in _lib.last_error()
+    # n = 0 is an empty batch: scalar checks only, NULL data pointers accepted, nothing launched
+    assert lib.dpi_sample_points(h, 0, 1, 0, 0, 1e-3, None, None) == 0
+    assert lib.dpi_point_baseline(h, n, None, 0, None, 0, None) == 0
+    assert lib.dpi_generate_with_gradients(h, n, None, 0, 4096, 50, 1, 0, 0, 3, 1e9, None, None, None, 0, None) == 0
+    assert lib.dpi_label_finalize(h, None, 0, 4096, 3, 1e9, None, None, 0, None) == 0
+    assert lib.dpi_sample_points(h, -1, 1, 0, 0, 1e-3, None, None) == _lib.DPI_ERR_ARG
+    assert lib.dpi_generate_with_gradients(h, n, None, -1, 4096, 50, 1, 0, 0, 3, 1e9, None, None, None, 0,
+                                           None) == _lib.DPI_ERR_ARG
     # estimator / precision settings validate their arguments
     assert lib.dpi_problem_set_estimate_delta_t(h, -0.1) == _lib.DPI_ERR_ARG
     assert lib.dpi_problem_set_estimate_delta_t(h, float("nan")) == _lib.DPI_ERR_ARG

@@ -444,3 +444,52 @@ def test_hessian_labels_shard_invariance_and_determinism():
     y = gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"))
     y1 = gen.generate_with_gradients_and_hessians(tx, point_base=0)
     assert torch.equal(y, y1)
+
+
+@pytest.mark.parametrize("kind", ["cha_mlp", "ou_pis", "gbm_hess"])
+def test_empty_and_single_point_batches(kind):
+    """Edge batches: n = 0 returns empty label blocks without launching (and without moving the
+    point counter); n = 1 (a one-point grid, a single-row PIS chunk) matches the oracle."""
+    import deeppicarditeration_amd as dpi
+    torch.manual_seed(5)
+    kw = dict(device="cuda:0", t_always_uniform=True, n_estimate_terminal=128, n_estimate_integral=128,
+              n_euler_steps=6, seed=9, epoch=1)
+    if kind == "cha_mlp":
+        eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+        net = _random_mlp(eq, [128] * 4, 5)
+        oeq, onet = O.Cha(100, 1.0, 5.0, 1.0), _oracle_mlp(net)
+    elif kind == "ou_pis":
+        eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+        net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+        oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+        onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    else:
+        eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+        net = _random_mlp(eq, [64] * 3, 5)
+        oeq, onet = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy()), _oracle_mlp(net)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, **kw)
+    nx, hess = eq.nx, kind == "gbm_hess"
+    width = 1 + nx + (nx * nx if hess else 0)
+    pb0 = gen.point_base
+    if hess:
+        tx0, y0 = gen.sample_with_gradients_and_hessians(0)
+    else:
+        tx0, y0 = gen.sample_with_gradients(0)
+    assert tuple(tx0.shape) == (0, 1 + nx) and tuple(y0.shape) == (0, width) and y0.is_cuda
+    assert gen.point_base == pb0
+    empty = torch.empty(0, 1 + nx, device="cuda:0")
+    y0 = gen.generate_with_gradients_and_hessians(empty) if hess else gen.generate_with_gradients(empty)
+    assert tuple(y0.shape) == (0, width)
+    torch.cuda.synchronize()
+
+    tx, _ = gen.sample_t_and_x(1, point_base=17)
+    if hess:
+        y = gen.generate_with_gradients_and_hessians(tx, point_base=17).cpu().numpy()
+        ref = O.labels_grad_hess(oeq, onet, tx.cpu().double().numpy(), 128, 6, 9, 1, 17)
+    else:
+        y = gen.generate_with_gradients(tx, point_base=17).cpu().numpy()
+        ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 6, 9, 1, 17)
+    parts = rel_l2_parts(y, ref)
+    print(kind, parts)
+    assert all(v < TOL for v in parts.values()), parts
