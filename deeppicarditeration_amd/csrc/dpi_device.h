@@ -151,6 +151,7 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ g, int ncol
 // lane of group q holds in the 16x16 C layout of tiles 2u and 2u+1, so activations become the B
 // operand without any data movement.
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32v4 __attribute__((ext_vector_type(4)));
 constexpr float SPLIT_LO = 2048.0f, SPLIT_INV = 1.0f / 2048.0f;
 
@@ -752,11 +753,14 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 // through W1x) and z_0 = W1x[:, d] stay fp32 from LDS; the adjoint reads the transposed split
 // weights (WTS) from L2 once.
 __device__ __forceinline__ void split8u(const float (&x)[8], half8& hi, half8& lo) {
+  typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 h = (_Float16)x[j];
-    hi[j] = h;
-    lo[j] = (_Float16)(x[j] - (float)h);
+  for (int j = 0; j < 8; j += 2) {
+    const f32x2 x2 = {x[j], x[j + 1]};
+    const half2v h = __builtin_convertvector(x2, half2v);
+    const half2v l = __builtin_convertvector(x2 - __builtin_convertvector(h, f32x2), half2v);
+    hi[j] = h.x, hi[j + 1] = h.y;
+    lo[j] = l.x, lo[j + 1] = l.y;
   }
 }
 template <int H, int L>
@@ -789,9 +793,10 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     for (int u = 0; u < NU; ++u) {
       float v[8];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = f[2 * u][r] * x[2 * u][r];
-        v[4 + r] = f[2 * u + 1][r] * x[2 * u + 1][r];
+      for (int r = 0; r < 4; r += 2) {
+        const f32x2 a = f32x2{f[2 * u][r], f[2 * u][r + 1]} * f32x2{x[2 * u][r], x[2 * u][r + 1]};
+        const f32x2 b = f32x2{f[2 * u + 1][r], f[2 * u + 1][r + 1]} * f32x2{x[2 * u + 1][r], x[2 * u + 1][r + 1]};
+        v[r] = a.x, v[r + 1] = a.y, v[4 + r] = b.x, v[5 + r] = b.y;
       }
       split8u(v, bh[u], bl[u]);
     }
@@ -897,18 +902,26 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
         if (l < L - 1) fz[l][T][r] = delu_from_a(act[l][T][r]) * bs;
       }
   }
-  // tangent sweep over the state dimensions
+  // tangent sweep over the state dimensions.  The lam z^2 terms accumulate in register pairs
+  // (v_pk_mul_f32 + v_pk_fma_f32: one VALU issue per unit instead of two).
   float s1 = 0.f, s2 = 0.f;
   for (int d = 0; d < e.nx; ++d) {
     float z[HT][4];
-    float term = 0.f;
+    f32x2 term2 = {0.f, 0.f};
+    auto acc_terms = [&](const float (&lm)[HT][4], const float (&zz)[HT][4]) {
+#pragma unroll
+      for (int T = 0; T < HT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 z2 = {zz[T][r], zz[T][r + 1]}, l2 = {lm[T][r], lm[T][r + 1]};
+          term2 = (l2 * z2) * z2 + term2;
+        }
+    };
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
-        term = fmaf(lam[0][T][r] * z[T][r], z[T][r], term);
-      }
+      for (int r = 0; r < 4; ++r) z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+    acc_terms(lam[0], z);
 #pragma unroll
     for (int l = 1; l < L; ++l) {
       half8 bh[NU], bl[NU];
@@ -918,12 +931,10 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int T = 0; T < HT; ++T)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          z[T][r] = o[T][r];
-          term = fmaf(lam[l][T][r] * o[T][r], o[T][r], term);
-        }
+        for (int r = 0; r < 4; ++r) z[T][r] = o[T][r];
+      acc_terms(lam[l], z);
     }
-    const float ud = qsum(term);
+    const float ud = qsum(term2.x + term2.y);
     const float c = (float)sh.cnt[d * P + pp];
     s1 = fmaf(c, ud, s1);
     s2 = fmaf(c, fabsf(ud), s2);
