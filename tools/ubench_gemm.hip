@@ -5,9 +5,11 @@
 // the max relative difference of each variant's output against the product kernel.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -369,6 +371,11 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
     mma(Fc);
     tw_mma += stamp() - b0;
   };
+  uint64_t clk0 = 0, rt0 = 0;
+  if constexpr (VAR & 1024) {  // in-kernel clock: s_memtime / s_memrealtime around the main loop
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   if constexpr (VAR & 128) {
     // branch-free steady state (nk even): the DMA of chunk min(u + 3, nk - 1) is issued every
     // iteration (the tail re-fetches the last chunk into free slots) so every wait is the same
@@ -399,6 +406,14 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
     for (int u = 0; u < nk; u += 2) {
       step(u, std::integral_constant<int, 0>{});
       if (u + 1 < nk) step(u + 1, std::integral_constant<int, 1>{});
+    }
+  }
+  if constexpr (VAR & 1024) {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* st = reinterpret_cast<unsigned long long*>(const_cast<float*>(AUX)) + 2 * blockIdx.x;
+      st[0] = clk1 - clk0;
+      st[1] = rt1 - rt0;
     }
   }
   if constexpr (VAR & 64) {
@@ -518,6 +533,217 @@ __global__ void k_convert_u(const float* in, float* out, int rows, int Kp, int l
     for (int j = 0; j < 8; ++j) v[j] *= scale;
     put8_u(reinterpret_cast<uint32_t*>(out + (size_t)m * ld) + 32 * u + 8 * q, v);
   }
+}
+
+// Measured negative result (kept for the record): the persistent form below is bitwise equal to
+// k_gemm_x3 but slower (262,144 rows: 575-605 vs 460-510 us; 32,768 rows: 84 vs 63 us) - the
+// tile-boundary stall it removes was not where the non-loop time goes, and its epilogue spills.
+namespace dpi {
+// Persistent form of k_gemm_x3: gridDim.x (a multiple of 8, at most one block per CU) blocks walk
+// the tiles v = blockIdx.x + j gridDim.x (the same XCD-aware remap of v), and the LDS ring and the
+// fragment double buffer run across tile boundaries: the next tile's first chunks are in flight
+// while this tile's last chunks multiply and its epilogue stores, so no tile pays the prologue's
+// memory latency or waits for a block slot.  Same products in the same order as k_gemm_x3 (bitwise
+// equal outputs).  Requires nk = Kp / 32 even.
+template <int EPI, int NT>
+__global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3p(int M, int Kp, int n_ntiles, int n_tiles,
+                                                            const uint32_t* __restrict__ W, float wscale,
+                                                            const float* __restrict__ X, int ldx,
+                                                            float* __restrict__ OUT, int ldc,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ AUX, int ldaux) {
+  static_assert(NT == 2 || NT == 4, "wave n-tiles");
+  constexpr int BN = 32 * NT, BM = X3_BM, STAGE = (BN + BM) * 32, NWAVE = X3_THREADS / 64;
+  constexpr int NINS = (BN + BM) / 8, PER_WAVE = NINS / NWAVE;
+  static_assert(NINS % NWAVE == 0 && (PER_WAVE == 6 || PER_WAVE == 5), "DMA split / vmcnt immediates");
+  __shared__ uint32_t sm[X3_STAGES * STAGE];
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int il = lane & 15, ql = lane >> 4;
+  const int G = gridDim.x, bid = blockIdx.x;
+  if (bid >= n_tiles) return;  // block-uniform
+  const int my_tiles = (n_tiles - 1 - bid) / G + 1;
+  const int nk = Kp >> 5, total = my_tiles * nk;
+  const int q8 = n_tiles >> 3, r8 = n_tiles & 7;
+  auto tile_of = [&](int j) {
+    const int v = bid + j * G, xcd = v & 7, loc = v >> 3;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  };
+  const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
+
+  auto issue = [&](int g, int slot) {  // global chunk g = j nk + c of this block's tile sequence
+    const int j = g / nk, c = g - j * nk, t = tile_of(j);
+    const int mt = t / n_ntiles, m0 = mt * BM, n0 = (t - mt * n_ntiles) * BN;
+    uint32_t* dst = sm + slot * STAGE;
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+      const int w = k * NWAVE + wv;
+      const int r = 8 * w + (lane >> 3);
+      const int gr = (lane & 7) ^ x3_swz(r);
+      const uint32_t* src;
+      if (r < BN)
+        src = W + (size_t)(n0 + r) * Kp + 32 * c + 4 * gr;
+      else
+        src = Xw + (size_t)min(m0 + r - BN, M - 1) * ldx + 32 * c + 4 * gr;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+    }
+  };
+  auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {
+    const int s = x3_swz(row);
+    const uint32_t* rp = buf + row * 32;
+    h = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql) ^ s)));
+    l = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql + 1) ^ s)));
+  };
+  auto vm_wait = [&]() {
+    if constexpr (PER_WAVE == 6)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  };
+  f4v acc[NT][4];
+  h8 ah[2][NT], al[2][NT], bh[2][4], bl[2][4];
+  auto load = [&](int slot, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    const uint32_t* buf = sm + slot * STAGE;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) frag(buf, wn * 16 * NT + 16 * t + il, ah[F][t], al[F][t]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) frag(buf, BN + wm * 64 + 16 * b + il, bh[F][b], bl[F][b]);
+  };
+  auto mma = [&](auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bl[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+      }
+  };
+  auto body = [&](int g, auto Fc) {  // g + 1 < total
+    constexpr int F = decltype(Fc)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    vm_wait();
+    __builtin_amdgcn_s_barrier();
+    issue(min(g + 3, total - 1), g % X3_STAGES);
+    load((g + 1) % X3_STAGES, std::integral_constant<int, F ^ 1>{});
+    mma(Fc);
+#pragma unroll
+    for (int i = 0; i < 2 * (NT + 4); ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3 * NT * 4 / (2 * (NT + 4)), 0);
+    }
+  };
+  issue(0, 0);
+  issue(min(1, total - 1), 1);
+  issue(min(2, total - 1), 2);
+  if constexpr (PER_WAVE == 6)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  load(0, std::integral_constant<int, 0>{});
+  int g = 0;
+  for (int j = 0; j < my_tiles; ++j) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[t][b] = f4v{0.f, 0.f, 0.f, 0.f};
+    const bool last = j + 1 == my_tiles;
+    const int gend = g + nk - 2;  // the tile's last pair starts here
+    for (; g < gend; g += 2) {
+      body(g, std::integral_constant<int, 0>{});
+      body(g + 1, std::integral_constant<int, 1>{});
+    }
+    body(g, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (!last) {  // chunk g + 1 without reading chunk g + 2 yet: the epilogue runs with one fragment set dead
+      vm_wait();
+      __builtin_amdgcn_s_barrier();
+      issue(min(g + 4, total - 1), (g + 1) % X3_STAGES);
+      mma(std::integral_constant<int, 1>{});
+    } else {
+      mma(std::integral_constant<int, 1>{});
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const int t = tile_of(j);
+    const int mt = t / n_ntiles, m0 = mt * BM, n0 = (t - mt * n_ntiles) * BN;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = m0 + wm * 64 + 16 * b + il;
+      if (m >= M) continue;
+#pragma unroll
+      for (int c = 0; c < NT / 2; ++c) {
+        const int U = (n0 >> 5) + wn * (NT / 2) + c;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * c][b][r] * wscale;
+          v[4 + r] = acc[2 * c + 1][b][r] * wscale;
+        }
+        if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
+          if (bias) {
+            const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
+            const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 16 + 4 * ql);
+            v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+            v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+          }
+          if (EPI == EPI_BIAS_ELU)
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) v[jj] = v[jj] > 0.f ? v[jj] : __expf(v[jj]) - 1.0f;
+        } else {
+          float a[8];
+          x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) v[jj] *= a[jj] > 0.f ? 1.0f : a[jj] + 1.0f;
+        }
+        x3_put8(OUT + (size_t)m * ldc, 0, U, ql, v);
+      }
+    }
+    if (!last) load((g + 2) % X3_STAGES, std::integral_constant<int, 0>{});  // the next tile's first chunk
+    g += 2;
+  }
+}
+
+}  // namespace dpi
+
+// in-kernel clock of the main loop (MI355X_MICROARCH.md DVFS item 6): the stamped variant runs
+// back to back for ~2 s, then the last launch's per-block (memtime, realtime) deltas give the clock
+// and the loop's cycles; MFMA share = 16 cycles x MFMAs per SIMD / loop cycles.
+template <int EPI, int VAR>
+void clock_u(const char* name, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, float* OUT,
+             const float* bias, float* STAMP) {
+  const int nnt = Np / 128, nmt = (M + X3_BM - 1) / X3_BM;
+  dim3 grid(nnt * nmt), block(X3_THREADS);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  int iters = 0;
+  float ms = 0.f;
+  CK(hipEventRecord(e0));
+  while (ms < 2000.f) {
+    for (int i = 0; i < 64; ++i)
+      hipLaunchKernelGGL((k_x3u<EPI, VAR>), grid, block, 0, 0, M, Kp, nnt, W, ws, X, Kp, OUT, Np, bias, STAMP, Np);
+    iters += 64;
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms, e0, e1));
+  }
+  std::vector<unsigned long long> st(2 * grid.x);
+  CK(hipMemcpy(st.data(), STAMP, st.size() * 8, hipMemcpyDeviceToHost));
+  std::vector<double> clk, cyc;
+  for (unsigned b = 0; b < grid.x; ++b) {
+    clk.push_back((double)st[2 * b] / (double)st[2 * b + 1] * 100.0);  // MHz
+    cyc.push_back((double)st[2 * b]);
+  }
+  std::sort(clk.begin(), clk.end());
+  std::sort(cyc.begin(), cyc.end());
+  const double mfma_cyc = 16.0 * 3.0 * 4.0 * 4.0 * (Kp / 32) * 2.0;  // per SIMD: 2 waves x nk x 48 MFMAs x 16
+  std::printf("%-34s %8.2f us/launch  clock %.0f MHz (median over blocks)  loop %.0f cycles  MFMA share %.2f\n",
+              name, ms * 1e3f / iters, clk[clk.size() / 2], cyc[cyc.size() / 2], mfma_cyc / cyc[cyc.size() / 2]);
 }
 
 template <int EPI, int VAR>
@@ -640,6 +866,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&OUT, (size_t)M * Np * 4));
   CK(hipMalloc(&REF, (size_t)M * Np * 4));
   CK(hipMalloc(&bias, Np * 4));
+  float* STAMP;
+  CK(hipMalloc(&STAMP, (size_t)(M / X3_BM + 1) * (Np / 128) * 16));
   hipLaunchKernelGGL(k_fill, dim3(Np), dim3(128), 0, 0, reinterpret_cast<float*>(W), Np, Kp, Kp, 7u, 0.05f);
   hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, X, M, Kp, Kp, 11u, 1.0f);
   hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, AUX, M, Np, Np, 13u, 1.5f);
@@ -678,6 +906,44 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     return ms * 1e3f / iters;
   };
+  auto prodp = [&](int epi, int iters, float* dst) {
+    const int nt = nnt * nmt, G = std::min(nt, 256);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) {
+      if (epi == 1)
+        hipLaunchKernelGGL((k_gemm_x3p<EPI_BIAS_ELU, 4>), dim3(G), dim3(X3_THREADS), 0, 0, M, Kp, nnt, nt, WU,
+                           1.0f / 16.0f, XU, Kp, dst, Np, bias, AUXU, Np);
+      else
+        hipLaunchKernelGGL((k_gemm_x3p<EPI_DELU, 4>), dim3(G), dim3(X3_THREADS), 0, 0, M, Kp, nnt, nt, WU,
+                           1.0f / 16.0f, XU, Kp, dst, Np, nullptr, AUXU, Np);
+    }
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e3f / iters;
+  };
+  auto cmp = [&](const char* name, float us) {
+    std::vector<float> a((size_t)M * Np), b((size_t)M * Np);
+    CK(hipMemcpy(a.data(), OUT, a.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), REF, b.size() * 4, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 0; i < a.size(); ++i) bad += (std::memcmp(&a[i], &b[i], 4) != 0);
+    std::printf("%s %8.2f us  %7.1f TF/s(eff f16)  words differing from k_gemm_x3: %zu\n", name, us,
+                2.0 * 3.0 * M * (double)Kp * Np / (us * 1e-6) / 1e12, bad);
+  };
+  for (int epi = 1; epi <= 2; ++epi) {
+    prod(epi, 1, REF);
+    CK(hipMemset(OUT, 0, (size_t)M * Np * 4));
+    prodp(epi, 1, OUT);
+    CK(hipDeviceSynchronize());
+    cmp(epi == 1 ? "elu  persistent k_gemm_x3p (-> OUT)" : "delu persistent k_gemm_x3p (-> OUT)", prodp(epi, 50, OUT));
+    std::printf("%s product k_gemm_x3 (-> OUT)       %8.2f us\n", epi == 1 ? "elu " : "delu", prod(epi, 50, OUT));
+    std::printf("%s persistent again (-> OUT)        %8.2f us\n", epi == 1 ? "elu " : "delu", prodp(epi, 50, OUT));
+  }
   for (int epi = 1; epi <= 2; ++epi) {
     prod(epi, 1);
     const float us = prod(epi, 50);
@@ -688,6 +954,7 @@ int main(int argc, char** argv) {
       report<EPI_BIAS_ELU, 4, 1>("elu  v1 (old loop, no epilogue)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
       report_u<EPI_BIAS_ELU, 128>("elu  W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
       report_u<EPI_BIAS_ELU, 129>("elu  W3 no epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
+      clock_u<EPI_BIAS_ELU, 128 + 1024>("elu  W3 + clock stamps", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, bias, STAMP);
       report_u<EPI_BIAS_ELU, 128 + 256>("elu  W3 epilogue = stores only", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
                                         bias, AUXU);
       report_u<EPI_BIAS_ELU, 128 + 512>("elu  W3 epilogue = VALU only", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
