@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <tuple>
 #include <type_traits>
 #include <vector>
 
@@ -276,6 +277,8 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
   __shared__ uint32_t sm[3 * STAGE];
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   typedef float f4v __attribute__((ext_vector_type(4)));
+  uint64_t rt_entry = 0;
+  if constexpr (VAR & 1024) rt_entry = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
   const int il = lane & 15, ql = lane >> 4;
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
@@ -408,13 +411,10 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
       if (u + 1 < nk) step(u + 1, std::integral_constant<int, 1>{});
     }
   }
+  uint64_t clk1 = 0, rt1 = 0;
   if constexpr (VAR & 1024) {
-    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {
-      unsigned long long* st = reinterpret_cast<unsigned long long*>(const_cast<float*>(AUX)) + 2 * blockIdx.x;
-      st[0] = clk1 - clk0;
-      st[1] = rt1 - rt0;
-    }
+    clk1 = __builtin_amdgcn_s_memtime();
+    rt1 = __builtin_amdgcn_s_memrealtime();
   }
   if constexpr (VAR & 64) {
     asm volatile("s_waitcnt lgkmcnt(0) vmcnt(0)" ::: "memory");
@@ -518,6 +518,17 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
         for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
       }
       put8_u(reinterpret_cast<uint32_t*>(OUT + (size_t)m * ldc) + 32 * U + 8 * ql, v);
+    }
+  }
+  if constexpr (VAR & 1024) {  // per-block timeline (wave 0): entry, loop start/end, epilogue end, hardware ids
+    const uint64_t rt_end = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* st = reinterpret_cast<unsigned long long*>(const_cast<float*>(AUX)) + 8 * blockIdx.x;
+      st[0] = clk1 - clk0;
+      st[1] = rt1 - rt0;
+      st[2] = rt_entry, st[3] = rt0, st[4] = rt1, st[5] = rt_end;
+      st[6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      st[7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
     }
   }
 }
@@ -732,15 +743,28 @@ void clock_u(const char* name, int M, int Kp, int Np, const uint32_t* W, float w
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
   }
-  std::vector<unsigned long long> st(2 * grid.x);
+  std::vector<unsigned long long> st(8 * grid.x);
   CK(hipMemcpy(st.data(), STAMP, st.size() * 8, hipMemcpyDeviceToHost));
-  std::vector<double> clk, cyc;
+  std::vector<double> clk, cyc, pro, loop, epi, tot, gap;
+  std::vector<std::tuple<unsigned long long, unsigned long long, unsigned long long, unsigned>> ev;
   for (unsigned b = 0; b < grid.x; ++b) {
-    clk.push_back((double)st[2 * b] / (double)st[2 * b + 1] * 100.0);  // MHz
-    cyc.push_back((double)st[2 * b]);
+    const unsigned long long* q = &st[8 * b];
+    clk.push_back((double)q[0] / (double)q[1] * 100.0);  // MHz
+    cyc.push_back((double)q[0]);
+    pro.push_back((q[3] - q[2]) * 10.0), loop.push_back((q[4] - q[3]) * 10.0), epi.push_back((q[5] - q[4]) * 10.0);
+    tot.push_back((q[5] - q[2]) * 10.0);  // ns (100 MHz realtime)
+    const unsigned long long hw = q[6];
+    const unsigned long long cu = (q[7] << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15);
+    ev.emplace_back(cu, q[2], q[5], b);
   }
-  std::sort(clk.begin(), clk.end());
-  std::sort(cyc.begin(), cyc.end());
+  std::sort(ev.begin(), ev.end());
+  for (size_t i = 1; i < ev.size(); ++i)
+    if (std::get<0>(ev[i]) == std::get<0>(ev[i - 1]))
+      gap.push_back(((double)std::get<1>(ev[i]) - (double)std::get<2>(ev[i - 1])) * 10.0);
+  for (auto* v : {&clk, &cyc, &pro, &loop, &epi, &tot, &gap}) std::sort(v->begin(), v->end());
+  auto med = [](const std::vector<double>& v) { return v.empty() ? 0.0 : v[v.size() / 2]; };
+  std::printf("  per block (median, ns): prologue %.0f  loop %.0f  epilogue %.0f  entry->end %.0f  same-CU gap %.0f "
+              "(%zu gaps)\n", med(pro), med(loop), med(epi), med(tot), med(gap), gap.size());
   const double mfma_cyc = 16.0 * 3.0 * 4.0 * 4.0 * (Kp / 32) * 2.0;  // per SIMD: 2 waves x nk x 48 MFMAs x 16
   std::printf("%-34s %8.2f us/launch  clock %.0f MHz (median over blocks)  loop %.0f cycles  MFMA share %.2f\n",
               name, ms * 1e3f / iters, clk[clk.size() / 2], cyc[cyc.size() / 2], mfma_cyc / cyc[cyc.size() / 2]);
@@ -867,7 +891,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&REF, (size_t)M * Np * 4));
   CK(hipMalloc(&bias, Np * 4));
   float* STAMP;
-  CK(hipMalloc(&STAMP, (size_t)(M / X3_BM + 1) * (Np / 128) * 16));
+  CK(hipMalloc(&STAMP, (size_t)(M / X3_BM + 1) * (Np / 128) * 64));
   hipLaunchKernelGGL(k_fill, dim3(Np), dim3(128), 0, 0, reinterpret_cast<float*>(W), Np, Kp, Kp, 7u, 0.05f);
   hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, X, M, Kp, Kp, 11u, 1.0f);
   hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, AUX, M, Np, Np, 13u, 1.5f);
