@@ -41,6 +41,8 @@ SIGNATURES = {
     "dpi_set_gemm_precision": (c_int, [c_int]),
     "dpi_workspace_bytes": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_sample_points": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_void_p, c_void_p]),
+    "dpi_sample_points_t": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int, c_void_p,
+                                    c_void_p]),
     "dpi_point_baseline": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "dpi_label_moments": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
                                   c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),

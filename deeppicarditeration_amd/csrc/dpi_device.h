@@ -1003,14 +1003,26 @@ __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh,
 // Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
 template <int KIND>
 __global__ void k_sample_points(EqDev e, int n, uint32_t k0, uint32_t k1, uint32_t c3t, uint32_t c3x0,
-                                uint32_t c3x, uint32_t point_base, float eps, float alpha_init_sqrt, float* tx) {
+                                uint32_t c3x, uint32_t point_base, float eps, int t_factors, float alpha_init_sqrt,
+                                float* tx) {
   const int nb = (e.nx + 3) >> 2;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = gid / nb, j = gid - i * nb;
   if (i >= n) return;
   const uint32_t ig = point_base + (uint32_t)i;
-  const float U = u01_co(philox4x32_10(0u, 0u, ig, c3t, k0, k1).x);
-  const float t = (e.T - 2.f * eps) * (1.f - U) + eps;
+  float t;
+  if (t_factors == 0) {  // sample_t_always_uniform (data.py:161-167)
+    const float U = u01_co(philox4x32_10(0u, 0u, ig, c3t, k0, k1).x);
+    t = (e.T - 2.f * eps) * (1.f - U) + eps;
+  } else {  // sample_t (data.py:149-159): T (1 - prod of t_factors uniforms), left to right
+    float prod = 1.f;
+    for (int r0 = 0; r0 < t_factors; r0 += 4) {
+      const auto w = philox4x32_10((uint32_t)(r0 >> 2), 0u, ig, c3t, k0, k1);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      for (int q = 0; q < 4 && r0 + q < t_factors; ++q) prod *= u01_co(ws[q]);
+    }
+    t = e.T * (1.f - prod);
+  }
   float* row = tx + (size_t)i * (1 + e.nx);
   if (j == 0) row[0] = t;
   const f4 z = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x, k0, k1));

@@ -882,7 +882,13 @@ extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) 
 
 extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
                       float* tx, void* stream) {
-  if (!p || (!tx && n) || n < 0 || epoch > 0xFFFFFFu) return fail(DPI_ERR_ARG, "sample_points: bad arguments");
+  return dpi_sample_points_t(p, n, seed, epoch, point_base, eps, 0, tx, stream);
+}
+
+extern "C" int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
+                                   int t_factors, float* tx, void* stream) {
+  if (!p || (!tx && n) || n < 0 || epoch > 0xFFFFFFu || t_factors < 0 || t_factors > 4096)
+    return fail(DPI_ERR_ARG, "sample_points: bad arguments (t_factors in [0, 4096])");
   if (n == 0) return 0;
   const int nb = (p->e.nx + 3) >> 2;
   const int total = n * nb;
@@ -893,15 +899,15 @@ extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t e
   switch (p->e.kind) {
     case DPI_EQ_CHA:
       hipLaunchKernelGGL(k_sample_points<DPI_EQ_CHA>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, p->alpha_init_sqrt, tx);
+                         eps, t_factors, p->alpha_init_sqrt, tx);
       break;
     case DPI_EQ_OU:
       hipLaunchKernelGGL(k_sample_points<DPI_EQ_OU>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, p->alpha_init_sqrt, tx);
+                         eps, t_factors, p->alpha_init_sqrt, tx);
       break;
     case DPI_EQ_GBM:
       hipLaunchKernelGGL(k_sample_points<DPI_EQ_GBM>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, p->alpha_init_sqrt, tx);
+                         eps, t_factors, p->alpha_init_sqrt, tx);
       break;
     default:
       return fail(DPI_ERR_UNSUPPORTED, "sample_points: equation kind");

@@ -65,8 +65,6 @@ class OnlineDataGenerator:
             raise AssertionError("Currently only SimpleDiffusionEquation and OUProcessEquation are supported")  # :426-429
         if equation.nu != 1:
             raise AssertionError("Currently only nu=1 is supported")
-        if not t_always_uniform:
-            raise NotImplementedError("t_always_uniform=False (product-of-uniforms t sampler) is not built yet")
         self.estimate_delta_t = float(estimate_delta_t or 0.0)
         if self.estimate_delta_t < 0:
             raise ValueError(f"estimate_delta_t must be >= 0 (got {estimate_delta_t})")
@@ -79,6 +77,10 @@ class OnlineDataGenerator:
         self.equation = equation
         self.solution = solution
         self.N, self.i = N, i
+        # t sampler (data.py:109-112): sample_t_always_uniform, or sample_t's product of N - i + 1 uniforms
+        self.t_factors = 0 if t_always_uniform else int(N) - int(i) + 1
+        if not 0 <= self.t_factors <= 4096:
+            raise ValueError(f"sample_t needs 1 <= N - i + 1 <= 4096 (N={N}, i={i})")
         self.T = float(equation.T)
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -135,11 +137,11 @@ class OnlineDataGenerator:
 
     # ------------------------------------------------------------------ reference entry points
     def sample_t_and_x(self, n_batch, point_base=None):
-        """sample_t_always_uniform + equation.sample_x (data.py:161-167, :211-217): tx (n, 1+nx)."""
+        """t_sampler + equation.sample_x (data.py:149-167, :211-217): tx (n, 1+nx)."""
         tx = torch.empty(n_batch, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
         pb = self._take_points(n_batch) if point_base is None else point_base
-        _lib.check(self.lib.dpi_sample_points(self.problem, n_batch, self.seed, self.epoch, pb, self.eps, _ptr(tx),
-                                              _stream(self.device)), "dpi_sample_points")
+        _lib.check(self.lib.dpi_sample_points_t(self.problem, n_batch, self.seed, self.epoch, pb, self.eps,
+                                                self.t_factors, _ptr(tx), _stream(self.device)), "dpi_sample_points_t")
         return tx, pb
 
     def sample_with_gradients(self, n_batch):

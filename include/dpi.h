@@ -19,6 +19,7 @@
  *   dpi_net_create_mlp       picard/solution.py:123-135   construct_mlp (state-dict order)
  *   dpi_net_create_pisgrad   picard/solution.py:138-289   PISGradNet (state-dict order)
  *   dpi_sample_points        picard/data.py:161-167, :211-217  sample_t_always_uniform + equation.sample_x
+ *   dpi_sample_points_t      picard/data.py:149-159 (sample_t, t_always_uniform: false) or :161-167
  *   dpi_point_baseline       picard/data.py:506-518, :918-920  g(x) and get_f(..., baseline_repeat=M)
  *   dpi_label_moments        picard/data.py:899-926 + :471-527 (+ :1226-1325 get_f) summed over MC paths
  *   dpi_label_finalize       picard/data.py:924-926, :525-526, :222  mean over M, + g(x), clip
@@ -139,6 +140,13 @@ size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
  * x = x0 + sqrt(t) sqrt(alpha) xi.  Point i uses counter c2 = point_base + i. */
 int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
                       float* tx, void* stream);
+
+/* dpi_sample_points with the t sampler chosen by t_factors (0 <= t_factors <= 4096):
+ * 0 = sample_t_always_uniform (as dpi_sample_points); R >= 1 = sample_t (t_always_uniform: false,
+ * picard/data.py:149-159), t = T (1 - U_0 U_1 ... U_{R-1}) with R = N - i + 1, U_r = word r&3 of
+ * Philox counter (r>>2, 0, point_base + i, DPI_TAG_T | epoch << 8), eps unused. */
+int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
+                        int t_factors, float* tx, void* stream);
 
 /* Per-point baseline g(x), f(t, x, u, grad u) (+ network terms) into the workspace. */
 int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes,

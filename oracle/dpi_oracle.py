@@ -283,11 +283,20 @@ class PISGradNet:
 
 
 # ----------------------------------------------------------------------------- sampling
-def sample_points(eq, n, seed, epoch=0, point_base=0, eps=EPS_T):
-    """Draws 1-3 of sample_with_gradients (picard/data.py:211-223)."""
+def sample_points(eq, n, seed, epoch=0, point_base=0, eps=EPS_T, t_factors=0):
+    """Draws 1-3 of sample_with_gradients (picard/data.py:211-223).  t_factors = 0:
+    sample_t_always_uniform (:161-167); t_factors = R = N - i + 1: sample_t (:149-159),
+    t = T (1 - prod of R uniforms), multiplied left to right."""
     i = point_base + np.arange(n)
-    u = px.uniforms(px.TAG_T, epoch, seed, i, 0)
-    t = ((eq.T - 2 * eps) * (1 - u) + eps)[:, None]                          # data.py:166-167
+    if t_factors:
+        u = px.uniforms_seq(px.TAG_T, epoch, seed, i, 0, t_factors)
+        prod = np.ones(n)
+        for r in range(t_factors):
+            prod = prod * u[:, r]
+        t = (eq.T * (1 - prod))[:, None]                                    # data.py:157-159
+    else:
+        u = px.uniforms(px.TAG_T, epoch, seed, i, 0)
+        t = ((eq.T - 2 * eps) * (1 - u) + eps)[:, None]                      # data.py:166-167
     if isinstance(eq, OUProcessEquation):
         x0 = eq.sample_x0(n, z=px.normals(px.TAG_X0, epoch, seed, i, 0, 0, eq.nx))
     else:
@@ -472,9 +481,10 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
     return y
 
 
-def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf, delta_t=0.0):
+def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf, delta_t=0.0,
+                          t_factors=0):
     """picard/data.py:211-223: (tx, clip(y))."""
-    tx = sample_points(eq, n, seed, epoch, point_base)
+    tx = sample_points(eq, n, seed, epoch, point_base, t_factors=t_factors)
     y = labels_grad(eq, net, tx, M, K, seed, epoch, point_base, v, delta_t=delta_t)
     return tx, np.clip(y, -sample_bound, sample_bound)
 

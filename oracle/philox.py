@@ -115,6 +115,15 @@ def uniforms(tag, epoch, seed, i, m, open_low=False):
     return uniform_oc(w0) if open_low else uniform_co(w0)
 
 
+def uniforms_seq(tag, epoch, seed, i, m, R):
+    """R uniforms [0, 1) per (i, m): word r&3 of counter (r>>2, m, i, c3); r = 0 is uniforms()."""
+    i, m = np.broadcast_arrays(np.asarray(i, np.int64), np.asarray(m, np.int64))
+    r = np.arange(R, dtype=np.int64)
+    words = philox4x32_10(r >> 2, m[..., None], i[..., None], c3_word(tag, epoch), seed)
+    w = np.stack(words, axis=-1)  # shape + (R, 4)
+    return uniform_co(w[..., r, r & 3])
+
+
 def randint_idx(tag, epoch, seed, i, m, v, high):
     """v indices in [0, high) per (i, m): word q&3 of counter (q>>2, m, i, c3), idx = (w*high)>>32."""
     i, m = np.broadcast_arrays(np.asarray(i, np.int64), np.asarray(m, np.int64))

@@ -151,9 +151,12 @@ class NoiseQueue:
         assert not self.items, f"{len(self.items)} injected draws unused"
 
 
-def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v):
+def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v, t_factors=0):
     i = point_base + np.arange(n)
-    items = [("rand", px.uniforms(px.TAG_T, epoch, seed, i, 0)[:, None])]
+    if t_factors:  # sample_t (data.py:149-159): torch.rand(n, N - i + 1)
+        items = [("rand", px.uniforms_seq(px.TAG_T, epoch, seed, i, 0, t_factors))]
+    else:
+        items = [("rand", px.uniforms(px.TAG_T, epoch, seed, i, 0)[:, None])]
     if eq_name == "OUProcessEquation":
         items.append(("randn", px.normals(px.TAG_X0, epoch, seed, i, 0, 0, nx)))
     items.append(("randn", px.normals(px.TAG_X, epoch, seed, i, 0, 0, nx)))
@@ -216,7 +219,8 @@ def state_dict_np(module):
 
 
 def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, point_base=0, v=0,
-             init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False, delta_t=0.0):
+             init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False, delta_t=0.0, picard_N=1,
+             picard_i=1, t_uniform=True):
     torch.set_default_dtype(torch.float64)
     eq = make_equation(eq_name, eq_kw, workdir)
     torch.manual_seed(init_seed)
@@ -235,7 +239,7 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
             net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
     hess = CfgNode({"method": "SDGD" if v > 0 else None, "kwargs": CfgNode({"v": v} if v > 0 else {})})
     gen = data.OnlineDataGenerator(
-        eq, net, 1, 1, device="cpu", t_always_uniform=True, n_estimate_terminal=M,
+        eq, net, picard_N, picard_i, device="cpu", t_always_uniform=t_uniform, n_estimate_terminal=M,
         n_estimate_integral=M, hessian_approximation=hess, sample_bound=None,
         estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=delta_t)
     if hessians:
@@ -243,13 +247,14 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
         with NoiseQueue(items):
             tx, y = gen.sample_with_gradients_and_hessians(n)
     else:
-        items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v)
+        t_factors = 0 if t_uniform else picard_N - picard_i + 1
+        items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v, t_factors)
         with NoiseQueue(items):
             tx, y = gen.sample_with_gradients(n)
     out = {
         "case": name, "eq": eq_name, "net": "zero" if zero else net_kind, "n": n, "M": M, "K": K,
         "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v, "hessians": hessians,
-        "delta_t": delta_t,
+        "delta_t": delta_t, "t_factors": 0 if (t_uniform or hessians) else picard_N - picard_i + 1,
         "tx": tx.numpy(), "y": y.detach().numpy(),
     }
     for k, val in eq_kw.items():
@@ -317,6 +322,13 @@ def main(only=None):
              v=100, workdir=wd, delta_t=0.4)
     run_case("td_ou_pis32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 6, 64, 2, 26, workdir=wd,
              delta_t=0.55)
+    # sample_t (t_always_uniform: false, data.py:149-159): t = T (1 - prod of N - i + 1 uniforms)
+    run_case("tprod_cha_mlp16_K2", "Cha", cha, "mlp", {"neurons": [16, 16]}, 6, 64, 2, 31, workdir=wd,
+             picard_N=5, picard_i=2, t_uniform=False)
+    run_case("tprod_ou_mlp16_K2", "OUProcessEquation", ou, "mlp", {"neurons": [16, 16]}, 5, 64, 2, 32, epoch=4,
+             workdir=wd, picard_N=3, picard_i=3, t_uniform=False)
+    run_case("tprod_gbm_mlp16_sdgd_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 5, 64, 1, 33,
+             v=100, workdir=wd, picard_N=9, picard_i=3, t_uniform=False)
     shutil.rmtree(wd)
 
 

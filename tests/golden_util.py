@@ -23,6 +23,11 @@ CASES = [c for c in _ALL if not _is_hess(c)]       # sample_with_gradients fixtu
 HESS_CASES = [c for c in _ALL if _is_hess(c)]      # sample_with_gradients_and_hessians fixtures
 
 
+def t_factors(f):
+    """0: sample_t_always_uniform; R = N - i + 1: sample_t's product of R uniforms (tprod_* fixtures)."""
+    return int(f["t_factors"]) if "t_factors" in f else 0
+
+
 def delta_t(f):
     """DATA.ESTIMATE_DELTA_T of a fixture (0 = the plain estimators; TD fixtures td_*)."""
     return float(f["delta_t"]) if "delta_t" in f else 0.0

@@ -3,7 +3,7 @@ import numpy as np
 import torch
 
 import deeppicarditeration_amd as dpi
-from golden_util import delta_t, state_dict
+from golden_util import delta_t, state_dict, t_factors
 
 
 def product_equation(f):
@@ -40,7 +40,9 @@ def generator(f, eq, module, M=None, K=None):
     M = int(f["M"]) if M is None else M
     v = int(f["v"])
     hess = {"method": "SDGD", "kwargs": {"v": v}} if v > 0 else None
-    return dpi.OnlineDataGenerator(eq, module, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+    R = t_factors(f)  # sample_t fixtures: a Picard (N, i) with N - i + 1 = R
+    return dpi.OnlineDataGenerator(eq, module, R if R else 1, 1, device="cuda:0", t_always_uniform=R == 0,
+                                   n_estimate_terminal=M,
                                    n_estimate_integral=M, n_euler_steps=int(f["K"]) if K is None else K,
                                    seed=int(f["seed"]), epoch=int(f["epoch"]), hessian_approximation=hess,
                                    estimate_delta_t=delta_t(f))

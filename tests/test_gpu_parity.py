@@ -22,7 +22,7 @@ def _need_gpu():
     L.load()  # fail loudly if the HIP library is missing
 
 
-from golden_util import CASES, delta_t, load, oracle_equation, oracle_net  # noqa: E402
+from golden_util import CASES, delta_t, load, oracle_equation, oracle_net, t_factors  # noqa: E402
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
@@ -40,19 +40,40 @@ def test_golden_reference_parity(case):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2"])
+@pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2", "tprod_cha_mlp16_K2", "tprod_gbm_mlp16_sdgd_K1"])
 def test_sample_points_match_oracle(case):
     f = load(case)
     eq = product_equation(f)
     gen = generator(f, eq, product_module(f, eq))
     n = 257
     tx, _ = gen.sample_t_and_x(n, point_base=int(f["point_base"]))
-    ref = O.sample_points(oracle_equation(f), n, int(f["seed"]), int(f["epoch"]), int(f["point_base"]))
+    ref = O.sample_points(oracle_equation(f), n, int(f["seed"]), int(f["epoch"]), int(f["point_base"]),
+                          t_factors=t_factors(f))
     tx = tx.cpu().double().numpy()
-    np.testing.assert_allclose(tx[:, 0], ref[:, 0], rtol=2e-7, atol=1e-7)
+    # fp32 t: one rounding for the uniform sampler, one per factor for sample_t's product
+    np.testing.assert_allclose(tx[:, 0], ref[:, 0], rtol=2e-6 if t_factors(f) else 2e-7, atol=1e-7)
     np.testing.assert_allclose(tx[:, 1:], ref[:, 1:], rtol=0, atol=2e-5)
     # the golden fixture's points came from the same contract
     np.testing.assert_allclose(tx[: int(f["n"])], f["tx"], rtol=0, atol=2e-5)
+
+
+@pytest.mark.parametrize("N,i", [(1, 1), (5, 2), (9, 3), (80, 1)])
+def test_product_t_sampler_matches_oracle(N, i):
+    """sample_t (t_always_uniform: false, data.py:149-159): t = T (1 - prod of N - i + 1 uniforms)
+    from the same Philox stream as the uniform sampler, x sampled at that t."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    gen = dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(1), N, i, device="cuda:0", t_always_uniform=False,
+                                  n_estimate_terminal=64, n_estimate_integral=64, n_euler_steps=1, seed=77, epoch=5)
+    n = 257
+    tx, _ = gen.sample_t_and_x(n, point_base=1000)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    ref = O.sample_points(oeq, n, 77, 5, 1000, t_factors=N - i + 1)
+    tx = tx.cpu().double().numpy()
+    np.testing.assert_allclose(tx[:, 0], ref[:, 0], rtol=2e-6, atol=1e-7)
+    np.testing.assert_allclose(tx[:, 1:], ref[:, 1:], rtol=0, atol=5e-5)
+    assert (tx[:, 0] > 0).all() and (tx[:, 0] <= 1.0).all()
 
 
 @pytest.mark.parametrize("case", ["cha_mlp16_K4", "ou_mlp16_K2", "gbm_mlp16_sdgd_K2"])
