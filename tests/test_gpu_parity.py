@@ -514,3 +514,40 @@ def test_empty_and_single_point_batches(kind):
     parts = rel_l2_parts(y, ref)
     print(kind, parts)
     assert all(v < TOL for v in parts.values()), parts
+
+
+@pytest.mark.parametrize("kind", ["cha_mlp", "ou_pis", "gbm_hess"])
+def test_label_call_captures_into_a_hip_graph(kind):
+    """include/dpi.h: label calls are stream-ordered, allocate nothing and never synchronise, so a
+    whole call (baseline, rollout / GEMM chain, reduce, finalize) captures into a hipGraph
+    (torch.cuda.graph) whose replays reproduce the eager labels bit for bit."""
+    import deeppicarditeration_amd as dpi
+    torch.manual_seed(8)
+    kw = dict(device="cuda:0", t_always_uniform=True, n_estimate_terminal=128, n_estimate_integral=128,
+              n_euler_steps=5, seed=12, epoch=2)
+    if kind == "cha_mlp":
+        eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+        net = _random_mlp(eq, [128] * 4, 8)
+    elif kind == "ou_pis":
+        eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+        net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    else:
+        eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+        net = _random_mlp(eq, [64] * 3, 8)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, **kw)
+    call = gen.generate_with_gradients_and_hessians if kind == "gbm_hess" else gen.generate_with_gradients
+    tx, _ = gen.sample_t_and_x(6, point_base=40)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        eager = call(tx, point_base=40).clone()  # also sizes the workspace before capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = call(tx, point_base=40)
+    for _ in range(3):
+        y.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, eager)
