@@ -62,25 +62,58 @@ class ShardedLabeler:
         return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
 
     # ------------------------------------------------------------------ two-phase (pipelined) labels
-    def begin(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
+    def prepare(self, n):
+        """Sample the next batch's points and their per-point baseline on a side stream, into one of
+        three workspaces, so both run while the current stream still executes the previous batch's
+        moments (the baseline is a handful of latency-bound blocks that otherwise serialise between
+        two path launches).  Returns the handle for begin(prepared=...)."""
+        gen = self.gen
+        cur = torch.cuda.current_stream(gen.device)
+        M = gen.n_estimate_integral
+        need = gen.workspace_bytes(n, M)
+        if getattr(self, "_prep_ws", None) is None or self._prep_ws[0].numel() < need:
+            torch.cuda.synchronize(gen.device)  # a resized pool must not alias in-flight work
+            self._side = torch.cuda.Stream(device=gen.device)
+            self._prep_ws = [torch.empty(need, dtype=torch.uint8, device=gen.device) for _ in range(3)]
+            self._prep_free, self._prep_next = [None] * 3, 0
+        k = self._prep_next
+        self._prep_next = (k + 1) % 3
+        ws = self._prep_ws[k]
+        with torch.cuda.stream(self._side):
+            if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
+                self._side.wait_event(self._prep_free[k])
+            tx, pb = gen.sample_t_and_x(n)
+            gen.point_baseline(tx, ws=ws)
+            ready = torch.cuda.Event()
+            ready.record(self._side)
+        tx.record_stream(cur)
+        return tx, pb, ws, ready, k
+
+    def begin(self, tx=None, point_base=None, flags=None, on_moments_begin=None, on_moments_end=None,
+              prepared=None):
         """First half of labels(): this rank's moments and, for world > 1, an asynchronous
         all-gather of them (RCCL runs on its own stream, so the caller can enqueue the next batch's
-        kernels while it is in flight).  Two workspaces alternate, so one batch may be pending
-        while the next begins.  Returns the handle end() turns into labels."""
+        kernels while it is in flight).  Two workspaces alternate (three with prepare()), so one
+        batch may be pending while the next begins.  Returns the handle end() turns into labels."""
         from . import _lib
         flags = _lib.DPI_BOTH if flags is None else flags
         M = self.gen.n_estimate_integral
         if self.gen.n_estimate_terminal != M:
             raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
-        n = tx.shape[0]
-        need = self.gen.workspace_bytes(n, M)
-        if not hasattr(self, "_ws_pool") or self._ws_pool[0].numel() < need:
-            dev = getattr(tx, "device", "cpu")
-            self._ws_pool = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self._ws_next = 0
-        ws = self._ws_pool[self._ws_next]
-        self._ws_next ^= 1
-        self.gen.point_baseline(tx, ws=ws)
+        slot = None
+        if prepared is not None:
+            tx, point_base, ws, ready, slot = prepared
+            torch.cuda.current_stream(self.gen.device).wait_event(ready)
+        else:
+            n = tx.shape[0]
+            need = self.gen.workspace_bytes(n, M)
+            if not hasattr(self, "_ws_pool") or self._ws_pool[0].numel() < need:
+                dev = getattr(tx, "device", "cpu")
+                self._ws_pool = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(2)]
+                self._ws_next = 0
+            ws = self._ws_pool[self._ws_next]
+            self._ws_next ^= 1
+            self.gen.point_baseline(tx, ws=ws)
         m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
@@ -88,20 +121,25 @@ class ShardedLabeler:
         if on_moments_end:
             on_moments_end()
         if self.world == 1:
-            return (ws, mom, None, None, flags, M)
+            return (ws, mom, None, None, flags, M, slot)
         import torch.distributed as dist
         mom = mom.contiguous()
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
         work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
-        return (ws, flat, work, tuple(mom.shape), flags, M)
+        return (ws, flat, work, tuple(mom.shape), flags, M, slot)
 
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
-        ws, mom, work, shape, flags, M = pending
+        ws, mom, work, shape, flags, M, slot = pending
         if work is not None:
             work.wait()  # the current stream waits for RCCL's, not the host
             mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
-        return self.gen.finalize(mom, M, flags, ws)
+        y = self.gen.finalize(mom, M, flags, ws)
+        if slot is not None:  # prepare() may refill this workspace once the finalize has run
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.gen.device))
+            self._prep_free[slot] = done
+        return y
 
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""

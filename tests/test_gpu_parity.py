@@ -551,3 +551,36 @@ def test_label_call_captures_into_a_hip_graph(kind):
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(y, eager)
+
+
+@pytest.mark.parametrize("kind", ["cha_mlp", "ou_pis"])
+def test_side_stream_preparation_equals_labels(kind):
+    """bench.py's pipeline: ShardedLabeler.prepare (sampling + per-point baseline on a side stream,
+    three rotating workspaces) -> begin -> end, with one batch in flight, gives every batch's labels
+    bit for bit as the one-stream labels() call on the same points."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+
+    def make():
+        torch.manual_seed(4)
+        if kind == "cha_mlp":
+            eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+            net = _random_mlp(eq, [128] * 4, 4)
+        else:
+            eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                       alpha_scale=4.0)
+            net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+        return dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True,
+                                       n_estimate_terminal=256, n_estimate_integral=256, n_euler_steps=6, seed=3)
+
+    lab, ref = ShardedLabeler(make()), ShardedLabeler(make())
+    got, pending = [], []
+    for _ in range(7):
+        pending.append(lab.begin(prepared=lab.prepare(16)))
+        if len(pending) > 1:
+            got.append(lab.end(pending.pop(0)))
+    got.append(lab.end(pending.pop(0)))
+    torch.cuda.synchronize()
+    for y in got:
+        tx, pb = ref.gen.sample_t_and_x(16)
+        assert torch.equal(y, ref.labels(tx, pb))
