@@ -176,6 +176,18 @@ class PicardRunner:
             u = net(tx).double().cpu()
         return float(torch.linalg.norm(u - exact) / torch.linalg.norm(exact))
 
+    def save_labels(self, tx, y):
+        """The reference's label file for this iteration: datasets `tx` and `u_ux` (`u_ux_uh` with
+        Hessian labels) of DATA.FLOAT, one file for the one label producer (worker 0)."""
+        import numpy as np
+        from .h5 import H5Saver, data_file
+        name = "u_ux_uh" if self.supervise_hessian else "u_ux"
+        dtype = np.float64 if str(self.cfg.DATA.FLOAT).lower() in ("double", "float64") else np.float32
+        saver = H5Saver(data_file(self.exp_dir, self.i, 0), tx.shape[0], [tx.shape[1], y.shape[1]], ["tx", name],
+                        dtype)
+        saver.save([tx, y], tx.shape[0])
+        saver.close()
+
     # ------------------------------------------------------------------ loop
     def run_one(self):
         self.i += 1
@@ -183,6 +195,8 @@ class PicardRunner:
         tx, y = self.labels()
         torch.cuda.synchronize(self.device)
         t_labels = time.perf_counter() - t0
+        if self.cfg.DATA.SAVE:  # data_iter_{i}/split_00.h5 (picard/data.py:1510-1525, data_saver.py:24-56)
+            self.save_labels(tx, y)
         net = self.new_network()
         if self.cfg.NETWORK.RELOAD and self.i > 1:  # picard_iteration.py:249-251
             net.load_state_dict(torch.load(self.checkpoint_path(self.i - 1), weights_only=True))

@@ -107,3 +107,36 @@ def test_picard_train_gbm_hessian_supervision(tmp_path):
     hist = runner.run()
     assert [h_["iter"] for h_ in hist] == [1, 2]
     assert all(h_["loss"] == h_["loss"] for h_ in hist) and all(h_["rel_l2_u"] is not None for h_ in hist)
+
+
+def test_picard_train_saves_reference_label_files(tmp_path):
+    """DATA.SAVE: true writes each iteration's labels as the reference's data_iter_{i}/split_00.h5
+    (datasets tx and u_ux, DATA.FLOAT), equal to the device labels of that iteration."""
+    import numpy as np
+    from deeppicarditeration_amd import h5
+    from deeppicarditeration_amd.h5 import H5Dataset, read_dataset
+    try:
+        h5._load()
+    except RuntimeError as e:
+        pytest.skip(str(e))
+    f = tmp_path / "cha.yaml"
+    f.write_text(CHA.format(name=tmp_path / "run_save").replace("  DATA_SIZE: 1024", "  DATA_SIZE: 1024\n  SAVE: true")
+                 .replace("PICARD: {N: 3}", "PICARD: {N: 2}"))
+    runner = PicardRunner(load_cfg(str(f)))
+    seen = {}
+    orig = runner.labels
+
+    def labels():
+        tx, y = orig()
+        seen[runner.i] = (tx.cpu().numpy(), y.cpu().numpy())
+        return tx, y
+
+    runner.labels = labels
+    runner.run()
+    for i in (1, 2):
+        p = tmp_path / "run_save" / f"data_iter_{i}" / "split_00.h5"
+        tx, y = read_dataset(p, "tx"), read_dataset(p, "u_ux")
+        assert tx.dtype == np.float32 and tx.shape == (1024, 9) and y.shape == (1024, 9)
+        assert np.array_equal(tx, seen[i][0]) and np.array_equal(y, seen[i][1])
+        batches = list(H5Dataset(p, 256, ["tx", "u_ux"]))
+        assert len(batches) == 4 and torch.equal(batches[1][1], torch.from_numpy(seen[i][1][256:512]))
