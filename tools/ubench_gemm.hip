@@ -448,6 +448,40 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_x3u(int M, int Kp, int n_ntil
     }
     return;
   }
+  if constexpr (VAR & 4096) {  // packed epilogue (ELU): v_pk_fma scale+bias, v_pk_mul log2e, pairs split
+    typedef _Float16 hh2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = m0 + wm * 64 + 16 * b + il;
+      if (m >= M) continue;
+#pragma unroll
+      for (int c = 0; c < NT / 2; ++c) {
+        const int U = (n0 >> 5) + wn * (NT / 2) + c;
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 16 + 4 * ql);
+        const f2v bb[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+        const f2v ws2 = {wscale, wscale};
+        u32x4_t hv, lv;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const auto& a = acc[2 * c + (p >> 1)][b];
+          const f2v x = {a[2 * (p & 1)], a[2 * (p & 1) + 1]};
+          f2v v = x * ws2 + bb[p];
+          const f2v tl = v * 1.4426950408889634f;
+          const f2v em = f2v{__builtin_amdgcn_exp2f(tl.x), __builtin_amdgcn_exp2f(tl.y)} - 1.0f;
+          v = f2v{v.x > 0.f ? v.x : em.x, v.y > 0.f ? v.y : em.y};
+          const hh2 h = __builtin_convertvector(v, hh2);
+          const hh2 l = __builtin_convertvector(v - __builtin_convertvector(h, f2v), hh2);
+          hv[p] = __builtin_bit_cast(uint32_t, h);
+          lv[p] = __builtin_bit_cast(uint32_t, l);
+        }
+        u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(OUT + (size_t)m * ldc) + 32 * U + 8 * ql);
+        g[0] = hv;
+        g[1] = lv;
+      }
+    }
+    return;
+  }
   if constexpr (VAR & 512) {  // epilogue VALU only: full math, one store per thread
     float sink = 0.f;
 #pragma unroll
@@ -978,6 +1012,11 @@ int main(int argc, char** argv) {
       report<EPI_BIAS_ELU, 4, 1>("elu  v1 (old loop, no epilogue)", M, Kp, Np, W, X, OUT, REF, bias, AUX);
       report_u<EPI_BIAS_ELU, 128>("elu  W3 (ubench copy)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
       report_u<EPI_BIAS_ELU, 129>("elu  W3 no epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
+      report_u<EPI_BIAS_ELU, 128 + 4096>("elu  W3 packed epilogue", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias,
+                                         AUXU);
+      report_u<EPI_BIAS_ELU, 128>("elu  W3 (again)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF, bias, AUXU);
+      report_u<EPI_BIAS_ELU, 128 + 4096>("elu  W3 packed epilogue (again)", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
+                                         bias, AUXU);
       clock_u<EPI_BIAS_ELU, 128 + 1024>("elu  W3 + clock stamps", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, bias, STAMP);
       report_u<EPI_BIAS_ELU, 128 + 256>("elu  W3 epilogue = stores only", M, Kp, Np, WU, 1.0f / 16.0f, XU, OUT, REF,
                                         bias, AUXU);
