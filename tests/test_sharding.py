@@ -229,3 +229,22 @@ def test_two_rank_gloo_hessian_labels_equal_single_rank():
     assert res[0].tobytes() == res[1].tobytes() == single.tobytes()
     ref = O.labels_grad_hess(eq, net, tx, MH, KH, 9)
     assert O.rel_l2(single, ref) < 1e-5
+
+
+def test_four_rank_gloo_labels_equal_single_rank():
+    """A 4-rank rehearsal of the N = 4 bench layout (M = 512 -> 128 MC indices per rank): every rank's
+    labels equal the single-rank labels bit for bit (M / (64 G) = 2, a power of two)."""
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    single = ShardedLabeler(OracleGen(eq, net), 0, 1).labels(tx, 0).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(4):
+        assert res[r].tobytes() == single.tobytes(), r
