@@ -53,6 +53,11 @@ __device__ __forceinline__ float tree_sum(const float* __restrict__ p, int cnt, 
 }
 
 // partial [n][2F][nbp] -> moments [n][2F] (and, if y != nullptr, the finalized labels).
+// torch.clip of the reference (data.py:222): NaN stays NaN (fmaxf alone would return -bound).
+__device__ __forceinline__ float clip_label(float v, float bound) {
+  return v != v ? v : fminf(fmaxf(v, -bound), bound);
+}
+
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
                                                 float* __restrict__ moments, const float* __restrict__ gx,
                                                 float invM, int add_g, float bound, float* __restrict__ y,
@@ -66,7 +71,7 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
     if (y && c < F) {
       float v = s * invM;
       if (c == 0 && add_g) v += gx[i];
-      y[(size_t)i * ystride + c] = fminf(fmaxf(v, -bound), bound);
+      y[(size_t)i * ystride + c] = clip_label(v, bound);
     }
   }
 }
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ h
   const float s = tree_sum(hpart + (size_t)i * nbp * C + c, nbp, (size_t)C);
   if ((threadIdx.x & 63) == 0) {
     if (hsum) hsum[(size_t)i * C + c] = s;
-    if (y) y[(size_t)i * ystride + yoff + c] = fminf(fmaxf(s * invM, -bound), bound);
+    if (y) y[(size_t)i * ystride + yoff + c] = clip_label(s * invM, bound);
   }
 }
 
@@ -92,7 +97,7 @@ __global__ void k_finalize_hess(const float* __restrict__ hsum, int n, int C, fl
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= (size_t)n * C) return;
   const size_t i = gid / C, c = gid - i * C;
-  y[i * ystride + yoff + c] = fminf(fmaxf(hsum[gid] * invM, -bound), bound);
+  y[i * ystride + yoff + c] = clip_label(hsum[gid] * invM, bound);
 }
 
 // parts [G][len] -> out [len]
@@ -111,7 +116,7 @@ __global__ void k_finalize_y(const float* moments, const float* gx, int n, int F
   const int i = gid / F, c = gid - i * F;
   float v = moments[(size_t)i * 2 * F + c] * invM;
   if (c == 0 && add_g) v += gx[i];
-  y[(size_t)i * ystride + c] = fminf(fmaxf(v, -bound), bound);
+  y[(size_t)i * ystride + c] = clip_label(v, bound);
 }
 
 __global__ void k_finalize(const float* moments, const float* gx, int n, int F, float invM, int add_g, float bound,
@@ -121,7 +126,7 @@ __global__ void k_finalize(const float* moments, const float* gx, int n, int F, 
   const int i = gid / F, c = gid - i * F;
   float v = moments[(size_t)i * 2 * F + c] * invM;
   if (c == 0 && add_g) v += gx[i];
-  y[gid] = fminf(fmaxf(v, -bound), bound);
+  y[gid] = clip_label(v, bound);
 }
 
 }  // namespace dpi

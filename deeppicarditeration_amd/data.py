@@ -24,7 +24,8 @@ from typing import Union
 import torch
 
 from . import _lib
-from .equations import Equation, OUProcessEquation, SimpleDiffusionEquation
+from .dataset import IterableDatasetWithInternalBatch
+from .equations import Equation, OUProcessEquation, SimpleDiffusionEquation, SimpleDiffusionEquationWithHessian
 from .solution import DeviceNet
 
 
@@ -82,8 +83,8 @@ class OnlineDataGenerator:
         if not 0 <= self.t_factors <= 4096:
             raise ValueError(f"sample_t needs 1 <= N - i + 1 <= 4096 (N={N}, i={i})")
         self.T = float(equation.T)
-        self.device = torch.device(device)
-        if self.device.type != "cuda":
+        self._device = torch.device(device)
+        if self._device.type != "cuda":
             raise ValueError("the HIP label generator runs on a GPU device ('cuda' on ROCm)")
         self.n_estimate_terminal = int(n_estimate_terminal)
         self.n_estimate_integral = int(n_estimate_integral)
@@ -121,13 +122,26 @@ class OnlineDataGenerator:
         _lib.check(self.lib.dpi_problem_set_estimate_delta_t(self.problem, self.estimate_delta_t),
                    "dpi_problem_set_estimate_delta_t")
 
+    @property
+    def device(self):
+        return self._device
+
+    def to(self, device):
+        """data.py:139-143, :433-436.  The labels are computed where the network weights were
+        uploaded; moving the generator to another device is not supported."""
+        d = torch.device(device)
+        if d.type != self._device.type or (d.index is not None and self._device.index is not None
+                                           and d.index != self._device.index):
+            raise NotImplementedError(f"the generator's device handle lives on {self._device}")
+        return self
+
     # ------------------------------------------------------------------ buffers
     def _workspace(self, n, M, hessians=False):
         need = self.lib.dpi_workspace_bytes(self.problem, self.net.handle, n, M)
         if hessians:
             need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self._device)
         return self._ws
 
     def _take_points(self, n):
@@ -138,10 +152,10 @@ class OnlineDataGenerator:
     # ------------------------------------------------------------------ reference entry points
     def sample_t_and_x(self, n_batch, point_base=None):
         """t_sampler + equation.sample_x (data.py:149-167, :211-217): tx (n, 1+nx)."""
-        tx = torch.empty(n_batch, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        tx = torch.empty(n_batch, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
         pb = self._take_points(n_batch) if point_base is None else point_base
         _lib.check(self.lib.dpi_sample_points_t(self.problem, n_batch, self.seed, self.epoch, pb, self.eps,
-                                                self.t_factors, _ptr(tx), _stream(self.device)), "dpi_sample_points_t")
+                                                self.t_factors, _ptr(tx), _stream(self._device)), "dpi_sample_points_t")
         return tx, pb
 
     def sample_with_gradients(self, n_batch):
@@ -174,10 +188,69 @@ class OnlineDataGenerator:
         pb = self._take_points(tx.shape[0]) if point_base is None else point_base
         return self._generate(self._as_points(tx), pb, _lib.DPI_INTEGRAL, bound=float("inf"))
 
+    def generate(self, tx, point_base=None):
+        """data.py:1203-1206: value-only labels, E g(X_T) + E int f(s, X_s, u) ds.  The reference's
+        value-only integral calls `equation.f(s, X, u)`, which every equation whose nonlinearity
+        reads the gradient or the Hessian defines as raising (equations.py:262-263, :369-370,
+        :575-576); so does this one, at call time."""
+        if self.equation.has_gradient_term or self.equation.has_hessian_term:
+            self.equation.f(None, None, None)  # raises the reference's NotImplementedError
+        raise NotImplementedError(f"{type(self.equation).__name__}: the device path has no value-only estimator")
+
+    def sample(self, n_batch):
+        """data.py:196-209: (tx, clip(u)) with u (n, 1)."""
+        tx, pb = self.sample_t_and_x(n_batch)
+        u = self.generate(tx, pb)
+        return tx, torch.clamp(u, -self.sample_bound, self.sample_bound)
+
+    # ------------------------------------------------------------------ exact labels (closed form)
+    def _t_x(self, n_batch):
+        tx, _ = self.sample_t_and_x(n_batch)
+        return tx, tx[:, :1], tx[:, 1:]
+
+    def sample_exact(self, n_batch):
+        """data.py:239-250: (tx, u*(t, x))."""
+        tx, t, x = self._t_x(n_batch)
+        with torch.no_grad():
+            return tx, self.equation.exact_solution(t, x).to(tx)
+
+    def sample_exact_with_gradients(self, n_batch):
+        """data.py:252-263: (tx, [u*, grad u*])."""
+        tx, t, x = self._t_x(n_batch)
+        with torch.no_grad():
+            u, ux = self.equation.u_u_x(t, x)
+        return tx, torch.cat([u.to(tx), ux.to(tx)], -1)
+
+    def sample_exact_with_gradients_and_hessians(self, n_batch):
+        """data.py:265-283: (tx, [u*, grad u*, Hess u*]) — equations with a Hessian term only."""
+        if not isinstance(self.equation, SimpleDiffusionEquationWithHessian):
+            raise AssertionError("exact Hessian labels need a SimpleDiffusionEquationWithHessian (data.py:274)")
+        tx, t, x = self._t_x(n_batch)
+        with torch.no_grad():
+            u, ux, uh = self.equation.u_u_x_u_hessian(t, x)
+        return tx, torch.cat([u.to(tx), ux.to(tx), uh.reshape(u.shape[0], -1).to(tx)], -1)
+
+    # ------------------------------------------------------------------ datasets (data.py:285-335)
+    def dataset(self, n_total, n_batch_buffer, batch_size):
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample)
+
     def dataset_with_gradients(self, n_total, n_batch_buffer, batch_size):
-        """data.py:291-297: the reference's buffered iterable dataset over sample_with_gradients."""
-        from .dataset import IterableDatasetWithInternalBatch
+        """The boundary: the buffered iterable dataset over sample_with_gradients."""
         return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
+
+    def dataset_with_gradients_and_hessians(self, n_total, n_batch_buffer, batch_size):
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size,
+                                                self.sample_with_gradients_and_hessians)
+
+    def dataset_exact(self, n_total, n_batch_buffer, batch_size):
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_exact)
+
+    def dataset_exact_with_gradients(self, n_total, n_batch_buffer, batch_size):
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients)
+
+    def dataset_exact_with_gradients_and_hessians(self, n_total, n_batch_buffer, batch_size):
+        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size,
+                                                self.sample_exact_with_gradients_and_hessians)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
     def workspace_bytes(self, n, M, hessians=False):
@@ -195,44 +268,44 @@ class OnlineDataGenerator:
         elif ws.numel() < self.workspace_bytes(n, M, hessians):
             raise ValueError("workspace too small")
         _lib.check(self.lib.dpi_point_baseline(self.problem, self.net.handle, _ptr(tx), n, _ptr(ws), ws.numel(),
-                                               _stream(self.device)), "dpi_point_baseline")
+                                               _stream(self._device)), "dpi_point_baseline")
         return ws
 
     def label_moments(self, tx, point_base, M, m_begin, m_end, flags, ws):
         """Sum / sum-of-squares of per-path contributions over m in [m_begin, m_end): (n, 2, 1+nx)."""
         n = tx.shape[0]
-        mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
         _lib.check(self.lib.dpi_label_moments(self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed,
                                               self.epoch, point_base, m_begin, m_end, flags, _ptr(mom), _ptr(ws),
-                                              ws.numel(), _stream(self.device)), "dpi_label_moments")
+                                              ws.numel(), _stream(self._device)), "dpi_label_moments")
         return mom
 
     def finalize(self, moments, M, flags, ws, bound=None):
         n = moments.shape[0]
-        y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+        y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
         b = self.sample_bound if bound is None else bound
         _lib.check(self.lib.dpi_label_finalize(self.problem, _ptr(moments), n, M, flags, b, _ptr(y), _ptr(ws),
-                                               ws.numel(), _stream(self.device)), "dpi_label_finalize")
+                                               ws.numel(), _stream(self._device)), "dpi_label_finalize")
         return y
 
     def label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
         """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2)."""
         n, nx = tx.shape[0], self.equation.nx
-        mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self.device)
-        hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self.device)
+        mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self._device)
+        hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
         _lib.check(self.lib.dpi_label_moments_hessians(
             self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, point_base, m_begin, m_end,
-            _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_label_moments_hessians")
+            _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self._device)), "dpi_label_moments_hessians")
         return mom, hs
 
     def finalize_hessians(self, moments, hsums, M, ws, bound=None):
         n, nx = moments.shape[0], self.equation.nx
-        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self.device)
+        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self._device)
         b = self.sample_bound if bound is None else bound
         _lib.check(self.lib.dpi_label_finalize_hessians(self.problem, _ptr(moments), _ptr(hsums), n, M, b, _ptr(y),
-                                                        _ptr(ws), ws.numel(), _stream(self.device)),
+                                                        _ptr(ws), ws.numel(), _stream(self._device)),
                    "dpi_label_finalize_hessians")
         return y
 
@@ -240,7 +313,7 @@ class OnlineDataGenerator:
         """(G, ...) per-rank sums -> (...), the canonical fixed-order tree over ranks."""
         parts = parts.contiguous()
         out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
-        _lib.check(self.lib.dpi_sums_reduce(_ptr(parts), parts.shape[0], out.numel(), _ptr(out), _stream(self.device)),
+        _lib.check(self.lib.dpi_sums_reduce(_ptr(parts), parts.shape[0], out.numel(), _ptr(out), _stream(self._device)),
                    "dpi_sums_reduce")
         return out
 
@@ -249,7 +322,7 @@ class OnlineDataGenerator:
         parts = parts.contiguous()
         G, n = parts.shape[0], parts.shape[1]
         out = torch.empty(parts.shape[1:], dtype=parts.dtype, device=parts.device)
-        _lib.check(self.lib.dpi_moments_reduce(_ptr(parts), G, n, self.equation.nx, _ptr(out), _stream(self.device)),
+        _lib.check(self.lib.dpi_moments_reduce(_ptr(parts), G, n, self.equation.nx, _ptr(out), _stream(self._device)),
                    "dpi_moments_reduce")
         return out
 
@@ -260,18 +333,18 @@ class OnlineDataGenerator:
         n, nx, M = tx.shape[0], self.equation.nx, self.n_estimate_integral
         need = self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M)
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self.device)
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self._device)
+        y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
         _lib.check(self.lib.dpi_generate_with_gradients_and_hessians(
             self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, bound, _ptr(y),
-            _ptr(self._ws), self._ws.numel(), _stream(self.device)), "dpi_generate_with_gradients_and_hessians")
+            _ptr(self._ws), self._ws.numel(), _stream(self._device)), "dpi_generate_with_gradients_and_hessians")
         return y
 
 
     def _as_points(self, tx):
-        if tx.device != self.device or tx.dtype != torch.float32 or not tx.is_contiguous():
-            tx = tx.to(device=self.device, dtype=torch.float32).contiguous()
+        if tx.device != self._device or tx.dtype != torch.float32 or not tx.is_contiguous():
+            tx = tx.to(device=self._device, dtype=torch.float32).contiguous()
         return tx
 
     def _generate(self, tx, pb, flags, bound=None):
@@ -281,13 +354,13 @@ class OnlineDataGenerator:
             M = MT if flags == _lib.DPI_TERMINAL else MI
             n = tx.shape[0]
             ws = self._workspace(n, max(MT, MI))
-            y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
-            self.last_moments = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self.device)
+            y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
+            self.last_moments = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
             b = self.sample_bound if bound is None else bound
             self._configure_problem()
             _lib.check(self.lib.dpi_generate_with_gradients(
                 self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, pb, flags, b, _ptr(y),
-                _ptr(self.last_moments), _ptr(ws), ws.numel(), _stream(self.device)), "dpi_generate_with_gradients")
+                _ptr(self.last_moments), _ptr(ws), ws.numel(), _stream(self._device)), "dpi_generate_with_gradients")
             return y
         ws = self.point_baseline(tx)
         yT = self.finalize(self.label_moments(tx, pb, MT, 0, MT, _lib.DPI_TERMINAL, ws), MT, _lib.DPI_TERMINAL, ws,

@@ -253,11 +253,31 @@ class OUProcessEquation(ComplexDiffusionEquation):
         var = self.var * et ** 2 + (float(self.alpha) / (2 * self.theta)) * (1 - et ** 2)
         return GaussianMixtureDiagonalCovariance(means, var, self.pi)
 
+    def _gmm_rows(self, t, x):
+        """Per-row GMM of the OU transition over T - t (get_gmm_t for every row at once):
+        component log-densities (n, K) and the scaled residuals diff/var (n, K, nx)."""
+        lam = (self.T - torch.as_tensor(t, dtype=x.dtype, device=x.device).reshape(-1, 1)).unsqueeze(-1)  # (n,1,1)
+        et = torch.exp(-self.theta * lam)
+        means = self.mu + (self.mean.to(x) - self.mu) * et                                    # (n,K,nx)
+        var = self.var.to(x) * et ** 2 + (float(self.alpha) / (2 * self.theta)) * (1 - et ** 2)
+        diff = x.unsqueeze(-2) - means
+        lp = (torch.log(self.pi.to(x)) - 0.5 * (self.nx * math.log(2.0 * math.pi) + torch.log(var).sum(-1))
+              - 0.5 * (diff ** 2 / var).sum(-1))
+        return lp, diff / var
+
     def exact_solution(self, t, x):
-        out = torch.empty(x.shape[0], 1, dtype=x.dtype, device=x.device)
-        for n in range(x.shape[0]):
-            out[n] = -self.get_gmm_t(self.T - float(t[n])).log_prob(x[n:n + 1])[0]
-        return out
+        """equations.py:650-652: -log of the OU-transported mixture at (T - t, x), row by row."""
+        lp, _ = self._gmm_rows(t, x)
+        return -torch.logsumexp(lp, dim=-1, keepdim=True)
+
+    def u_x(self, t, x):
+        """equations.py:668-681 (autograd there): grad_x of -log sum_k pi_k N_k = sum_k w_k (x - m_k)/v_k."""
+        lp, r = self._gmm_rows(t, x)
+        return torch.einsum("nk,nkd->nd", torch.softmax(lp, dim=-1), r)
+
+    def u_u_x(self, t, x):  # equations.py:697-700
+        lp, r = self._gmm_rows(t, x)
+        return -torch.logsumexp(lp, dim=-1, keepdim=True), torch.einsum("nk,nkd->nd", torch.softmax(lp, dim=-1), r)
 
     def _create_device_problem(self, lib):
         h = _lib.c_void_p()
@@ -311,6 +331,18 @@ class GBMEquationComplexExact(SimpleDiffusionEquationWithHessian):
 
     def laplacian(self, t, x):
         return -torch.sin(self._arg(t, x)) @ (self.v * (self.w[:, 1:] ** 2).sum(-1, keepdim=True)).to(x)
+
+    def u_u_x(self, t, x):  # equations.py:440-443
+        return self.exact_solution(t, x), self.u_x(t, x)
+
+    def u_hessian(self, t, x):
+        """equations.py:445-450: -sum_k v_k w_k w_k^T sin(w_k . [t, x]), (n, nx, nx)."""
+        wx = self.w[:, 1:].to(x)
+        return torch.einsum("nk,kij->nij", -torch.sin(self._arg(t, x)),
+                            self.v.to(x).reshape(-1, 1, 1) * wx.unsqueeze(2) * wx.unsqueeze(1))
+
+    def u_u_x_u_hessian(self, t, x):  # equations.py:381-385
+        return self.exact_solution(t, x), self.u_x(t, x), self.u_hessian(t, x)
 
     def hess_diag(self, t, x):
         return -torch.sin(self._arg(t, x)) @ (self.v * self.w[:, 1:] ** 2).to(x)

@@ -1,8 +1,11 @@
 """CLI of the reference (`picard train <cfg.yaml> [KEY VAL ...]`, picard/main.py:12-23):
 
+    picard train scripts/burgers/base_100d_T1.0_w0.0_0.yaml PICARD.N 2
     python -m deeppicarditeration_amd.main train scripts/burgers/base_100d_T1.0_w0.0_0.yaml PICARD.N 2
+    torchrun --nproc-per-node 8 -m deeppicarditeration_amd.main train <cfg.yaml>   (MC-sharded labels)
 """
 import argparse
+import os
 import sys
 from pathlib import Path
 
@@ -17,7 +20,21 @@ def train(argv):
     from .config import load_cfg
     from .runner import PicardRunner
     cfg = load_cfg(a.configfile, [x.lstrip("-") for x in a.overrides])
-    PicardRunner(cfg).run()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        PicardRunner(cfg).run()
+        return
+    # torchrun --nproc-per-node G -m deeppicarditeration_amd.main train cfg.yaml: one process per GPU,
+    # RCCL ("nccl" on ROCm) for the label moments' all-gather and the weight broadcast
+    import torch
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    try:
+        PicardRunner(cfg, device=f"cuda:{local}", rank=dist.get_rank(), world=dist.get_world_size()).run()
+    finally:
+        dist.destroy_process_group()
 
 
 def main(argv=None):

@@ -19,24 +19,28 @@ import json
 import pathlib
 import shutil
 import time
+import warnings
 
 import torch
 
 from . import equations as eqs
 from .config import CfgNode
 from .data import OnlineDataGenerator
+from .dataset import TensorDatasetBuiltInShuffle
+from .fit import build_objective, make_optimizer, train_steps
+from .sharding import ShardedLabeler
 from .solution import PISGradNet, ZeroSolution, construct_mlp
 
 
 class LabelBuffer:
-    """Device-resident (tx, y) label store for one Picard iteration; y is (u, u_x) or, with
-    hessians=True, (u, u_x, u_xx) of generate_with_gradients_and_hessians (data.py:225-237)."""
+    """Device-resident (tx, y) label store for one Picard iteration, filled by DATA_SIZE / POINTS_PER_CALL
+    calls of a batch_data_generator `sample(n) -> (tx, y)` (a generator's sample_with_gradients /
+    sample_with_gradients_and_hessians / sample_exact_*, or a ShardedLabeler's)."""
 
-    def __init__(self, gen, n_total, points_per_call, hessians=False):
-        self.gen = gen
+    def __init__(self, sample, n_total, points_per_call):
+        self.sample = sample
         self.n_total = int(n_total)
         self.ppc = max(1, min(int(points_per_call), self.n_total))
-        self.sample = gen.sample_with_gradients_and_hessians if hessians else gen.sample_with_gradients
 
     def fill(self):
         txs, ys = [], []
@@ -50,17 +54,47 @@ class LabelBuffer:
         return torch.cat(txs), torch.cat(ys)
 
 
+def eval_metrics(u, u_exact, ux=None, ux_exact=None, uxx=None, uxx_exact=None):
+    """EvalCallback.on_validation_epoch_start (picard/utils.py:404-475): MSE / rRMSE / rMAE / MArE of
+    u, and with gradients (EVAL.TEST_GRAD) / Hessians (EVAL.TEST_HESSIAN) the per-dimension
+    relative errors averaged over dimensions (suffix g / h).  numpy fp64 arrays."""
+    import numpy as np
+    err = np.abs(u - u_exact)
+    m = {"MSE": float(np.sqrt((err ** 2).mean())), "rRMSE": float(np.sqrt((err ** 2).sum()) / np.sqrt((u_exact ** 2).sum())),
+         "rMAE": float(err.sum() / np.abs(u_exact).sum()), "MArE": float((err / np.abs(u_exact)).mean())}
+    for tag, a, b in (("g", ux, ux_exact), ("h", uxx, uxx_exact)):
+        if a is None:
+            continue
+        e = np.abs(a - b)
+        m.update({f"MSE{tag}": float(np.sqrt((e ** 2).mean(0)).mean()),
+                  f"rRMSE{tag}": float((np.sqrt((e ** 2).sum(0)) / np.sqrt((b ** 2).sum(0))).mean()),
+                  f"rMAE{tag}": float((e.sum(0) / np.abs(b).sum(0)).mean()),
+                  f"MArE{tag}": float((e / np.abs(b)).mean())})
+    return m
+
+
 class PicardRunner:
-    def __init__(self, cfg: CfgNode, device="cuda"):
+    def __init__(self, cfg: CfgNode, device="cuda", rank=0, world=1, group=None):
+        """rank / world > 1: one process per GPU in a torch.distributed job (RCCL on the GPU).
+        Every rank generates the labels of its Monte-Carlo shard (ShardedLabeler: one all-gather of
+        label moments per call, identical labels on every rank); rank 0 fits, writes the checkpoint,
+        history and label files, and broadcasts the fitted weights, so every rank starts the next
+        Picard iteration from the same u."""
         self.cfg = cfg
         self.device = torch.device(device)
+        self.rank, self.world, self.group = int(rank), int(world), group
         self.exp_dir = pathlib.Path(cfg.NAME)
-        if self.exp_dir.exists() and any(self.exp_dir.iterdir()):
-            if not cfg.FORCE:
-                raise FileExistsError(f"Experiment directory {self.exp_dir} already exists.")
-            shutil.rmtree(self.exp_dir)
-        self.exp_dir.mkdir(parents=True, exist_ok=True)
-        (self.exp_dir / "config.yaml").write_text(cfg.dump())
+        if self.rank == 0:
+            if self.exp_dir.exists() and any(self.exp_dir.iterdir()):
+                if not cfg.FORCE:
+                    raise FileExistsError(f"Experiment directory {self.exp_dir} already exists.")
+                shutil.rmtree(self.exp_dir)
+            self.exp_dir.mkdir(parents=True, exist_ok=True)
+            (self.exp_dir / "config.yaml").write_text(cfg.dump())
+        if str(cfg.DATA.FLOAT).lower() in ("double", "float64"):  # picard/config.py:194-200
+            warnings.warn("DATA.FLOAT: double — the device label path computes in fp32 (labels within the "
+                          "north star's rel-L2 <= 1e-4 of the fp64 reference, DESIGN.md); the fit and the "
+                          "label files follow DATA.FLOAT", stacklevel=2)
         if cfg.METHOD.cls != "Picard":  # Diffusion / PINN / FullyNonlinearSolver baselines: out of scope
             raise NotImplementedError(f"METHOD.cls={cfg.METHOD.cls}: only the DPI (Picard) method is built")
         if cfg.PICARD.FORMULA == "TwoLayer":
@@ -88,93 +122,91 @@ class PicardRunner:
         return self.exp_dir / f"model_{i}.pt"
 
     # ------------------------------------------------------------------ labels
-    def labels(self):
+    def make_generator(self, solution, **overrides):
+        """PicardDataModule.get_data_generator (picard/data.py:1465-1496) on the device path."""
         d = self.cfg.DATA
-        kw = dict(d.kwargs)
-        gen = OnlineDataGenerator(
-            self.equation, self.u_current, self.N, self.i, device=self.device, **kw,
-            hessian_approximation=d.HESSIAN_APPROXIMATION, sample_bound=d.SAMPLE_BOUND,
-            estimate_terminal=d.ESTIMATE_TERMINAL, estimate_integral=d.ESTIMATE_INTEGRAL,
-            estimate_delta_t=d.ESTIMATE_DELTA_T, n_euler_steps=d.EULER_STEPS, seed=d.SEED)
-        return LabelBuffer(gen, d.DATA_SIZE, d.POINTS_PER_CALL, hessians=self.supervise_hessian).fill()
+        kw = dict(dict(d.kwargs), hessian_approximation=d.HESSIAN_APPROXIMATION, sample_bound=d.SAMPLE_BOUND,
+                  estimate_terminal=d.ESTIMATE_TERMINAL, estimate_integral=d.ESTIMATE_INTEGRAL,
+                  estimate_delta_t=d.ESTIMATE_DELTA_T, n_euler_steps=d.EULER_STEPS, seed=d.SEED)
+        kw.update(overrides)
+        return OnlineDataGenerator(self.equation, solution, self.N, self.i, device=self.device, **kw)
+
+    def label_sampler(self, gen):
+        """The batch_data_generator get_dataset_details would pick (data.py:1620-1661): exact labels
+        under DATA.EXACT, Monte-Carlo labels otherwise (MC-sharded over the ranks when world > 1)."""
+        hess = self.supervise_hessian
+        if self.cfg.DATA.EXACT:
+            return gen.sample_exact_with_gradients_and_hessians if hess else gen.sample_exact_with_gradients
+        src = gen
+        if self.world > 1:
+            src = ShardedLabeler(gen, self.rank, self.world, self.group)
+        return src.sample_with_gradients_and_hessians if hess else src.sample_with_gradients
+
+    def labels(self):
+        gen = self.make_generator(self.u_current)
+        d = self.cfg.DATA
+        return LabelBuffer(self.label_sampler(gen), d.DATA_SIZE, d.POINTS_PER_CALL).fill()
 
     # ------------------------------------------------------------------ fit
     def fit(self, net, tx, y):
+        """TRAIN.N_EPOCHS passes over the labels in BATCH_SIZE batches with the objective the
+        reference's solution wrapper computes (fit.build_objective; losses pinned against the
+        reference's training steps by tests/test_fit_golden.py).  As in the reference's data
+        module, the first epoch takes the labels in the order they were drawn and later epochs
+        replay the in-memory cache, shuffled when DATA.SHUFFLE is set (dataset.py:203-255)."""
         t = self.cfg.TRAIN
-        opt = getattr(torch.optim, t.OPTIMIZER.cls)(net.parameters(), **dict(t.OPTIMIZER.kwargs))
-        beta = float(t.LOSS.beta)
-        loss_fn = torch.square
-        if t.LOSS.FN.cls is not None:  # LossFnLinearClip (solution.py:22-33)
-            clip = float(t.LOSS.FN.kwargs["clip"])
-            loss_fn = lambda x: torch.where(x.abs() < clip, x * x, 2 * clip * x.abs() - clip ** 2)  # noqa: E731
-        gw, hw = 0.0, 0.0
-        kw = t.LOSS.SCALER.kwargs
-        if self.supervise_hessian:  # FixedHessianLossScaler (solution_jac.py:85-109)
-            if t.LOSS.SCALER.cls != "FixedHessianLossScaler":
-                raise NotImplementedError("SUPERVISE_HESSIAN needs LOSS.SCALER.cls = FixedHessianLossScaler")
-            gw, hw = float(kw["fixed_gradient_weight"]), float(kw["fixed_hessian_weight"])
-        elif self.supervise_gradient and t.LOSS.SCALER.cls == "FixedLossScaler":
-            gw = float(kw.get("fixed_weight", 0.0))
-        elif self.supervise_gradient and t.LOSS.SCALER.cls is not None:
-            raise NotImplementedError(f"loss scaler {t.LOSS.SCALER.cls}")
-        nx = self.equation.nx
-        n_hess_samples = int(t.NUM_HESS_SAMPLES)
-        hess_fn = None
-        if self.supervise_hessian:  # vmap(hessian(forward)) (solution_jac.py:128)
-            hess_fn = torch.func.vmap(torch.func.hessian(lambda z: net(z[None])[0, 0]))
+        objective, self.fit_kind = build_objective(t, self.equation.nx, self.supervise_gradient,
+                                                   self.supervise_hessian)
+        opt, sched = make_optimizer(net.parameters(), t.OPTIMIZER)
         n = tx.shape[0]
         bs = int(t.BATCH_SIZE) if t.BATCH_SIZE else n
-        last = float("nan")
-        for _ in range(int(t.N_EPOCHS)):
-            perm = torch.randperm(n, device=tx.device)
-            for b0 in range(0, n, bs):
-                idx = perm[b0:b0 + bs]
-                xb, yb = tx[idx].detach(), y[idx]
-                w = torch.exp(xb[:, :1] * beta)
-                if self.supervise_hessian:  # PicardSolutionGradientHessianWrapper (solution_jac.py:219-259)
-                    xb.requires_grad_(True)
-                    u = net(xb)
-                    ux = torch.autograd.grad(u.sum(), xb, create_graph=True)[0][:, 1:]
-                    uh = hess_fn(xb)[:, 1:, 1:].reshape(xb.shape[0], nx * nx)
-                    diff = uh - yb[:, 1 + nx:]
-                    if n_hess_samples > 0:
-                        idx_h = torch.randperm(nx * nx, device=xb.device)[:n_hess_samples]
-                        diff = diff[:, idx_h]
-                    v_loss = torch.mean(w * loss_fn(u - yb[:, :1]))
-                    g_loss = torch.mean(w * loss_fn(ux - yb[:, 1:1 + nx]), dim=0).sum()
-                    h_loss = torch.mean(w * loss_fn(diff), dim=0).sum()
-                    loss = v_loss + gw * g_loss + hw * h_loss
-                elif gw > 1e-9:  # PicardSolutionGradientWrapper (solution_jac.py:167-213)
-                    xb.requires_grad_(True)
-                    u = net(xb)
-                    ux = torch.autograd.grad(u.sum(), xb, create_graph=True)[0][:, 1:]
-                    v_loss = torch.mean(w * loss_fn(u - yb[:, :1]))
-                    g_loss = torch.mean(w * loss_fn(ux - yb[:, 1:1 + nx]), dim=0).sum()
-                    loss = v_loss + gw * g_loss
-                else:  # PicardBaseSolution.training_step (solution.py:75-82)
-                    loss = torch.mean(w * loss_fn(net(xb) - yb[:, :1]))
-                opt.zero_grad(set_to_none=True)
-                loss.backward()
-                opt.step()
-                last = float(loss.detach())
-        return last
+        losses = []
+        for epoch in range(int(t.N_EPOCHS)):
+            batches = TensorDatasetBuiltInShuffle(tx, y, batch_size=bs,
+                                                  shuffle=bool(self.cfg.DATA.SHUFFLE) and epoch > 0)
+            losses.append(train_steps(net, objective, opt, batches, sched))
+        losses = torch.cat(losses) if losses else torch.empty(0)
+        return float(losses[-1]) if losses.numel() else float("nan")
 
     # ------------------------------------------------------------------ eval
     def evaluate(self, net, n_points=None):
-        """rel-L2 of u against the exact solution on freshly sampled points (utils.py:410-476)."""
-        n = int(n_points or min(self.cfg.EVAL.L2_N_POINTS, 4096))
-        gen = OnlineDataGenerator(self.equation, ZeroSolution(1), self.N, self.i, device=self.device,
-                                  t_always_uniform=True, n_estimate_terminal=64, n_estimate_integral=64,
-                                  n_euler_steps=1, seed=self.cfg.DATA.SEED + 7919, epoch=0xFFFFFF - self.i)
-        tx, _ = gen.sample_t_and_x(n)
-        t, x = tx[:, :1].double().cpu(), tx[:, 1:].double().cpu()
+        """EvalCallback (picard/utils.py:329-478): at t = linspace(0, T, n) and x = equation.sample_x(t)
+        (seeded per iteration), u of the network vs the exact solution; with EVAL.TEST_GRAD the
+        gradient errors and with EVAL.TEST_HESSIAN the Hessian errors (at most 256 points for the
+        nx^2 Hessians).  Returns the metrics dict, or {} when the equation has no exact solution."""
+        import numpy as np
+        ev = self.cfg.EVAL
+        n = int(n_points or ev.L2_N_POINTS)
+        eq = self.equation
+        with torch.random.fork_rng(devices=[]):
+            torch.manual_seed(int(self.cfg.DATA.SEED) * 7919 + self.i)
+            t = torch.linspace(0.0, float(eq.T), n, dtype=torch.float64).reshape(n, 1)
+            x = eq.sample_x(t).to(torch.float64)
         try:
-            exact = self.equation.exact_solution(t, x)
+            u_exact = eq.exact_solution(t, x)
         except (NotImplementedError, AttributeError):
-            return None
-        with torch.no_grad():
-            u = net(tx).double().cpu()
-        return float(torch.linalg.norm(u - exact) / torch.linalg.norm(exact))
+            return {}
+        dt = next(net.parameters()).dtype if any(True for _ in net.parameters()) else torch.float32
+        tx = torch.cat([t, x], -1).to(device=self.device, dtype=dt)
+        grads = bool(ev.TEST_GRAD)
+        with torch.enable_grad() if grads else torch.no_grad():
+            if grads:
+                tx.requires_grad_(True)
+            u = net(tx)
+            ux = torch.autograd.grad(u.sum(), tx)[0][:, 1:] if grads else None
+        out = {"u": u.detach().double().cpu().numpy(), "u_exact": u_exact.numpy()}
+        if grads:
+            out.update(ux=ux.double().cpu().numpy(), ux_exact=eq.u_x(t, x).detach().numpy())
+            if ev.TEST_HESSIAN and hasattr(eq, "u_hessian"):
+                k = min(n, 256)
+                h = torch.func.vmap(torch.func.hessian(lambda z: net(z[None])[0, 0]))(tx[:k].detach())
+                out.update(uxx=h[:, 1:, 1:].reshape(k, -1).double().cpu().numpy(),
+                           uxx_exact=eq.u_hessian(t[:k], x[:k]).reshape(k, -1).numpy())
+        m = eval_metrics(out["u"], out["u_exact"], out.get("ux"), out.get("ux_exact"))
+        if "uxx" in out:
+            m.update({k: v for k, v in eval_metrics(out["u"][:1], out["u_exact"][:1], out["uxx"],
+                                                    out["uxx_exact"]).items() if k.endswith("h")})
+        return m
 
     def save_labels(self, tx, y):
         """The reference's label file for this iteration: datasets `tx` and `u_ux` (`u_ux_uh` with
@@ -191,26 +223,37 @@ class PicardRunner:
     # ------------------------------------------------------------------ loop
     def run_one(self):
         self.i += 1
+        sync = (lambda: torch.cuda.synchronize(self.device)) if self.device.type == "cuda" else (lambda: None)
+        sync()
         t0 = time.perf_counter()
         tx, y = self.labels()
-        torch.cuda.synchronize(self.device)
+        sync()
         t_labels = time.perf_counter() - t0
-        if self.cfg.DATA.SAVE:  # data_iter_{i}/split_00.h5 (picard/data.py:1510-1525, data_saver.py:24-56)
-            self.save_labels(tx, y)
         net = self.new_network()
-        if self.cfg.NETWORK.RELOAD and self.i > 1:  # picard_iteration.py:249-251
-            net.load_state_dict(torch.load(self.checkpoint_path(self.i - 1), weights_only=True))
-        t1 = time.perf_counter()
-        loss = self.fit(net, tx, y)
-        t_fit = time.perf_counter() - t1
-        torch.save(net.state_dict(), self.checkpoint_path(self.i))
-        rel = self.evaluate(net)
-        rec = {"iter": self.i, "labels": int(tx.shape[0]), "label_s": t_labels, "fit_s": t_fit, "loss": loss,
-               "rel_l2_u": rel}
-        self.history.append(rec)
-        with open(self.exp_dir / "history.jsonl", "a") as f:
-            f.write(json.dumps(rec) + "\n")
-        print(json.dumps(rec), flush=True)
+        rec = None
+        if self.rank == 0:
+            if self.cfg.DATA.SAVE:  # data_iter_{i}/split_00.h5 (picard/data.py:1510-1525, data_saver.py:24-56)
+                self.save_labels(tx, y)
+            if self.cfg.NETWORK.RELOAD and self.i > 1:  # picard_iteration.py:249-251
+                net.load_state_dict(torch.load(self.checkpoint_path(self.i - 1), weights_only=True))
+            t1 = time.perf_counter()
+            loss = self.fit(net, tx, y)
+            t_fit = time.perf_counter() - t1
+            torch.save(net.state_dict(), self.checkpoint_path(self.i))
+            metrics = self.evaluate(net)
+            M = int(dict(self.cfg.DATA.kwargs).get("n_estimate_integral", 1))
+            n = int(tx.shape[0])
+            rec = {"iter": self.i, "labels": n, "label_s": t_labels, "labels_per_s": n / t_labels,
+                   "path_labels_per_s": None if self.cfg.DATA.EXACT else n * M / t_labels, "ranks": self.world,
+                   "fit_s": t_fit, "fit": self.fit_kind, "loss": loss, "rel_l2_u": metrics.get("rRMSE"), **metrics}
+            self.history.append(rec)
+            with open(self.exp_dir / "history.jsonl", "a") as f:
+                f.write(json.dumps(rec) + "\n")
+            print(json.dumps(rec), flush=True)
+        if self.world > 1:  # every rank continues from rank 0's fit
+            import torch.distributed as dist
+            for v in net.state_dict().values():
+                dist.broadcast(v, src=0, group=self.group)
         self.u_current = net  # frozen by the next OnlineDataGenerator (data.py:409-412)
         return True
 

@@ -75,9 +75,12 @@ class ShardedLabeler:
             torch.cuda.synchronize(gen.device)  # a resized pool must not alias in-flight work
             self._side = torch.cuda.Stream(device=gen.device)
             self._prep_ws = [torch.empty(need, dtype=torch.uint8, device=gen.device) for _ in range(3)]
-            self._prep_free, self._prep_next = [None] * 3, 0
+            self._prep_free, self._prep_next, self._prep_busy = [None] * 3, 0, [False] * 3
         k = self._prep_next
+        if self._prep_busy[k]:
+            raise RuntimeError("prepare(): all three workspaces hold batches whose end() has not run")
         self._prep_next = (k + 1) % 3
+        self._prep_busy[k] = True
         ws = self._prep_ws[k]
         with torch.cuda.stream(self._side):
             if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
@@ -100,7 +103,7 @@ class ShardedLabeler:
         M = self.gen.n_estimate_integral
         if self.gen.n_estimate_terminal != M:
             raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
-        slot = None
+        slot = wslot = None
         if prepared is not None:
             tx, point_base, ws, ready, slot = prepared
             torch.cuda.current_stream(self.gen.device).wait_event(ready)
@@ -108,10 +111,16 @@ class ShardedLabeler:
             n = tx.shape[0]
             need = self.gen.workspace_bytes(n, M)
             if not hasattr(self, "_ws_pool") or self._ws_pool[0].numel() < need:
+                if any(getattr(self, "_ws_busy", ())):
+                    raise RuntimeError("begin(): cannot resize the workspaces while a batch is pending")
                 dev = getattr(tx, "device", "cpu")
                 self._ws_pool = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(2)]
-                self._ws_next = 0
-            ws = self._ws_pool[self._ws_next]
+                self._ws_next, self._ws_busy = 0, [False, False]
+            wslot = self._ws_next
+            if self._ws_busy[wslot]:
+                raise RuntimeError("begin(): two batches are already pending; end() one before beginning another")
+            self._ws_busy[wslot] = True
+            ws = self._ws_pool[wslot]
             self._ws_next ^= 1
             self.gen.point_baseline(tx, ws=ws)
         m0, m1 = self.shard(M)
@@ -121,16 +130,16 @@ class ShardedLabeler:
         if on_moments_end:
             on_moments_end()
         if self.world == 1:
-            return (ws, mom, None, None, flags, M, slot)
+            return (ws, mom, None, None, flags, M, slot, wslot)
         import torch.distributed as dist
         mom = mom.contiguous()
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
         work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
-        return (ws, flat, work, tuple(mom.shape), flags, M, slot)
+        return (ws, flat, work, tuple(mom.shape), flags, M, slot, wslot)
 
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
-        ws, mom, work, shape, flags, M, slot = pending
+        ws, mom, work, shape, flags, M, slot, wslot = pending
         if work is not None:
             work.wait()  # the current stream waits for RCCL's, not the host
             mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
@@ -139,6 +148,9 @@ class ShardedLabeler:
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.gen.device))
             self._prep_free[slot] = done
+            self._prep_busy[slot] = False
+        if wslot is not None:  # stream order makes the next user of this workspace run after finalize
+            self._ws_busy[wslot] = False
         return y
 
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
@@ -157,3 +169,14 @@ class ShardedLabeler:
             on_moments_end()
         mom = self.gather_moments(mom)
         return self.gen.finalize(mom, M, flags, ws)
+
+    # ------------------------------------------------------------------ batch_data_generator surface
+    def sample_with_gradients(self, n_batch):
+        """OnlineDataGenerator.sample_with_gradients with this rank's MC shard: every rank draws the
+        same points (same counters) and returns the same (tx, clip(u_ux))."""
+        tx, pb = self.gen.sample_t_and_x(n_batch)
+        return tx, self.labels(tx, pb)
+
+    def sample_with_gradients_and_hessians(self, n_batch):
+        tx, pb = self.gen.sample_t_and_x(n_batch)
+        return tx, self.labels_hessians(tx, pb)

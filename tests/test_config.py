@@ -86,3 +86,18 @@ def test_runner_rejects_out_of_scope_methods(tmp_path):
                                     "METHOD: {cls: Diffusion}\n")
     with pytest.raises(NotImplementedError):
         PicardRunner(load_cfg(f), device="cpu")
+
+
+
+def test_picard_console_entry_point(capsys):
+    """pyproject.toml exposes `picard` -> deeppicarditeration_amd.main:main (reference pyproject.toml:25-26)."""
+    import importlib
+    import tomli
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "pyproject.toml"), "rb") as f:
+        target = tomli.load(f)["project"]["scripts"]["picard"]
+    mod, fn = target.split(":")
+    main = getattr(importlib.import_module(mod), fn)
+    assert main([]) == 2 and "picard train" in capsys.readouterr().out
+    with pytest.raises(SystemExit):
+        main(["train", "/nonexistent.yaml"])

@@ -124,6 +124,22 @@ def test_two_rank_gloo_two_phase_pipeline_equals_labels():
         assert res[r][1].tobytes() == single_b.tobytes()
 
 
+def test_begin_refuses_a_third_pending_batch():
+    """Two workspaces alternate: a third begin() before any end() would overwrite a pending
+    batch's per-point baseline, so it raises; after one end() the pipeline continues."""
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    lab = ShardedLabeler(OracleGenTwoPhase(eq, net), 0, 1)
+    pa = lab.begin(tx, 0)
+    pb = lab.begin(tx, 100)
+    with pytest.raises(RuntimeError, match="pending"):
+        lab.begin(tx, 200)
+    lab.end(pa)
+    pc = lab.begin(tx, 200)
+    lab.end(pb)
+    lab.end(pc)
+
+
 def test_shard_ranges():
     from deeppicarditeration_amd.sharding import ShardedLabeler
     assert [ShardedLabeler(None, r, 4).shard(4096) for r in range(4)] == [(0, 1024), (1024, 2048), (2048, 3072),
