@@ -17,7 +17,6 @@ moments are combined with one all-gather over RCCL + dpi_moments_reduce.
 import argparse
 import json
 import os
-import platform
 import sys
 import time
 from pathlib import Path
@@ -93,12 +92,9 @@ def _make(wl, dpi):
     return eq, net
 
 
-def cpu_baseline(wl, sample_paths, target_s=10.0):
-    """Time the CPU oracle (oracle/: numpy fp64 restatement) on a bounded sample of the same
-    workload: whole points of `sample_paths` paths x K, same network, until ~target_s seconds."""
+def _oracle_objects(wl, eq, net):
+    """The CPU oracle's equation and network for a workload (fp64 numpy, oracle/dpi_oracle.py)."""
     from oracle import dpi_oracle as O
-    import deeppicarditeration_amd as dpi
-    eq, net = _make(wl, dpi)
     if wl["eq"] == "Cha":
         oeq = O.Cha(NX, 1.0, 5.0, 1.0)
     elif wl["eq"] == "OUProcessEquation":
@@ -108,10 +104,67 @@ def cpu_baseline(wl, sample_paths, target_s=10.0):
     if wl.get("pis"):
         onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
     else:
-        lin = [l for l in net if isinstance(l, torch.nn.Linear)]
-        onet = O.MLP([l.weight.detach().double().numpy() for l in lin], [l.bias.detach().double().numpy() for l in lin],
+        lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+        onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
                      ["ELU"] * (len(lin) - 1))
+    return oeq, onet
+
+
+def live_parity(wl, eq, net, tx, pb, y, M):
+    """rel-L2 of the first point of the first timed batch against the fp64 oracle on the same
+    counters (all M paths, K steps): value column and gradient block (and Hessian block)."""
+    import numpy as np
+    from oracle import dpi_oracle as O
+    oeq, onet = _oracle_objects(wl, eq, net)
+    t0 = time.perf_counter()
+    txr = tx[:1].double().cpu().numpy()
+    if wl.get("hess"):
+        ref = O.labels_grad_hess(oeq, onet, txr, M, wl["K"], 1, 1, pb, m_chunk=256)
+    else:
+        ref = O.labels_grad(oeq, onet, txr, M, wl["K"], 1, 1, pb, v=wl["sdgd"], m_chunk=512)
+    got = y[:1].double().cpu().numpy()
+    r = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(b))  # noqa: E731
+    out = {"value": r(got[:, :1], ref[:, :1]), "grad": r(got[:, 1:1 + NX], ref[:, 1:1 + NX])}
+    if wl.get("hess"):
+        out["hessian"] = r(got[:, 1 + NX:], ref[:, 1 + NX:])
+    out.update(tolerance=1e-4, what=f"first point of the first timed batch (point index {pb}), {M} paths x "
+                                    f"K={wl['K']} vs the fp64 oracle (oracle/dpi_oracle.py) on the same Philox counters",
+               oracle_s=round(time.perf_counter() - t0, 2))
+    return out
+
+
+def cpu_baseline(wl, sample_paths, target_s=6.0):
+    """The reference's label algorithm on the host cores (oracle/torch_cpu.py: estimate_terminal_
+    with_gradients + estimate_integral_with_gradients vectorised in PyTorch, pinned to the
+    reference's outputs by tests/test_cpu_baseline.py), same equation / network / M, in fp32 and
+    fp64 on all the CPUs this process may use.  GBM's Hessian nonlinearity: the fp64 numpy oracle
+    on one thread (its SDGD Hessian is not restated in torch)."""
+    import deeppicarditeration_amd as dpi
+    from oracle import torch_cpu as TC
+    eq, net = _make(wl, dpi)
+    cores = TC.host_cores()
+    model = TC.cpu_model()
+    if wl["eq"] in ("Cha", "OUProcessEquation"):
+        from oracle import dpi_oracle as O
+        oeq, _ = _oracle_objects(wl, eq, net)
+
+        def points(n, base):
+            return torch.from_numpy(O.sample_points(oeq, n, seed=1, point_base=base))
+        M = wl["m_per_gpu"]
+        res = {}
+        for dt, name in ((torch.float32, "fp32"), (torch.float64, "fp64")):
+            v, pts, secs, th = TC.time_reference_algorithm(eq, net, points, M, dt, target_s=target_s,
+                                                           points_per_call=1 if wl.get("pis") else 4, threads=cores)
+            res[name] = {"value": v, "points": pts, "seconds": round(secs, 2)}
+        return {"value": res["fp32"]["value"], "unit": "path-labels/s", "cores": cores, "kind": "port",
+                "dtype": "fp32", "fp64": res["fp64"]["value"], "cpu": model,
+                "sample": f"oracle/torch_cpu.py: the reference's estimators (data.py:471-527, 899-926; one Gaussian "
+                          f"jump per path, autograd grad u) in PyTorch on {cores} host threads, {M} paths per point; "
+                          f"fp32 {res['fp32']['points']} points in {res['fp32']['seconds']} s, fp64 "
+                          f"{res['fp64']['points']} points in {res['fp64']['seconds']} s"}
+    from oracle import dpi_oracle as O
     from threadpoolctl import threadpool_limits
+    oeq, onet = _oracle_objects(wl, eq, net)
     done, pts = 0, 0
     t0 = time.perf_counter()
     with threadpool_limits(limits=1):  # the restatement is a scalar port: one thread, BLAS included
@@ -127,10 +180,9 @@ def cpu_baseline(wl, sample_paths, target_s=10.0):
             dt = time.perf_counter() - t0
             if dt >= target_s:
                 break
-    return {"value": done / dt, "unit": "path-labels/s", "cores": 1, "kind": "port",
+    return {"value": done / dt, "unit": "path-labels/s", "cores": 1, "kind": "port", "dtype": "fp64", "cpu": model,
             "sample": f"oracle/dpi_oracle.py labels_grad, fp64 numpy, 1 thread, {pts} point(s) x {sample_paths} "
-                      f"paths x K={wl['K']} of this workload, {dt:.1f} s on "
-                      f"{platform.processor() or platform.machine()} (os.cpu_count={os.cpu_count()})"}
+                      f"paths x K={wl['K']} of this workload, {dt:.1f} s"}
 
 
 def main():
@@ -178,30 +230,47 @@ def main():
     pipelined = (world > 1 or args.pipelined or args.prepare) and not wl.get("hess")
     pending = []
 
+    # (tx, point_base) of every begun batch, in order; the labels come out in the same order.  The
+    # first timed batch's points and labels are kept for the parity check after the timed region.
+    begun, capture = [], {}
+
+    def finish(handle):
+        y = handle[1] if isinstance(handle[0], str) else labeler.end(handle)
+        tx_, pb_ = begun.pop(0)
+        if capture.get("armed") and "y" not in capture:
+            capture.update(tx=tx_, pb=pb_, y=y)
+        return y
+
     def step():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if args.prepare and pipelined:  # next batch's sampling + baseline on a low-priority side stream
-            pending.append(labeler.begin(prepared=labeler.prepare(N_POINTS), on_moments_begin=lambda: e0.record(),
+            prep = labeler.prepare(N_POINTS)
+            begun.append(prep[:2])
+            pending.append(labeler.begin(prepared=prep, on_moments_begin=lambda: e0.record(),
                                          on_moments_end=lambda: e1.record()))
             ev.append((e0, e1))
-            return labeler.end(pending.pop(0)) if len(pending) > 1 else None
+            return finish(pending.pop(0)) if len(pending) > 1 else None
         tx, pb = gen.sample_t_and_x(N_POINTS)
+        begun.append((tx, pb))
         if wl.get("hess"):
-            y = labeler.labels_hessians(tx, pb, on_moments_begin=lambda: e0.record(),
-                                        on_moments_end=lambda: e1.record())
+            pending.append(("hess", labeler.labels_hessians(tx, pb, on_moments_begin=lambda: e0.record(),
+                                                            on_moments_end=lambda: e1.record())))
+            y = finish(pending.pop(0))
         elif pipelined:
             pending.append(labeler.begin(tx, pb, on_moments_begin=lambda: e0.record(),
                                          on_moments_end=lambda: e1.record()))
-            y = labeler.end(pending.pop(0)) if len(pending) > 1 else None
+            y = finish(pending.pop(0)) if len(pending) > 1 else None
         else:
-            y = labeler.labels(tx, pb, on_moments_begin=lambda: e0.record(), on_moments_end=lambda: e1.record())
+            pending.append(("done", labeler.labels(tx, pb, on_moments_begin=lambda: e0.record(),
+                                                   on_moments_end=lambda: e1.record())))
+            y = finish(pending.pop(0))
         ev.append((e0, e1))
         return y
 
     def drain():
         y = None
         while pending:
-            y = labeler.end(pending.pop(0))
+            y = finish(pending.pop(0))
         return y
 
     # Clock ramp: the GPU needs ~10 ms of load to leave its idle clocks, which a 20-step run at
@@ -228,6 +297,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    capture["armed"] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         y = step()
@@ -242,6 +312,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, k_ms = float(t[0]), float(t[1])
     assert torch.isfinite(y).all()
+    parity = live_parity(wl, eq, net, capture["tx"], capture["pb"], capture["y"], M) if rank == 0 else None
     # Noise floor of the same launch (untimed, after the timed region): the identical rollout with
     # u = 0 (ZeroSolution: same Philox streams, same K-step EM, no network), i.e. the
     # Philox4x32-10 + Box-Muller VALU issue the noise contract fixes.
@@ -296,10 +367,12 @@ def main():
                        "schedule": ("two-phase, next batch prepared on a side stream" if args.prepare and pipelined
                                     else "two-phase (all-gather overlapped)" if pipelined else "one labels() call"),
                        "prewarm_steps": prewarm,
-                       "rel_l2_vs_ref": "1e-8 - 1.7e-6 measured (value / gradient / Hessian blocks), tolerance 1e-4 "
-                                        "(tests/test_gpu_parity.py)"},
+                       "rel_l2_vs_ref": parity},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak, "traffic": traffic,
+                         "traffic_source": (f"profile_derived: profiles/traffic_{args.workload}.json (rocprofv3 PMC "
+                                            "FETCH_SIZE / WRITE_SIZE passes of this bench command, HBM bytes per "
+                                            "label call)") if traffic is not None else None,
                          "peak_basis": peak_basis, "kernel": wl["kernel"],
                          "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
         }

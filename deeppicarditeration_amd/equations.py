@@ -220,6 +220,9 @@ class ComplexDiffusionEquation(DiffusionEquation):
         x_next = x + torch.sqrt(s - t) * self.alpha_sqrt.to(x) * dW
         return (x_next, dW) if return_dW else x_next
 
+    def f(self, t, x, y):  # equations.py:575-576
+        raise NotImplementedError("The equation has dependence on z, use fff or ff instead.")
+
     def fff(self, t, x, y, z):
         return self.ff(t, x, y, self.alpha_sqrt.to(z) * z)
 
@@ -296,6 +299,9 @@ class SimpleDiffusionEquationWithHessian(SimpleDiffusionEquation):
     has_gradient_term = True
     has_laplacian_term = False
     has_hessian_term = True
+
+    def f(self, t, x, y):  # equations.py:369-370
+        raise NotImplementedError("The equation has dependence on z and hessian, use ffh instead.")
 
 
 class GBMEquationComplexExact(SimpleDiffusionEquationWithHessian):

@@ -1,0 +1,110 @@
+"""CPU baseline for bench.py (test / measurement infrastructure, never on the product path): the
+reference's own label algorithm, vectorised in PyTorch on the host cores, as the reference runs it
+on a CPU — `estimate_terminal_with_gradients` (picard/data.py:899-926) + `estimate_integral_with_
+gradients` (:471-527) with `get_f` (:1226-1325) for equations whose nonlinearity is ff(t, x, u, grad u)
+(Cha, OUProcessEquation): one Gaussian jump per path (the reference's sampler, equations.py:217-230),
+u and grad u of the network by autograd, the per-point baseline f(t, x) evaluated once and repeated.
+
+The equations and networks are the torch modules of deeppicarditeration_amd (the plugin interface),
+evaluated on the CPU in fp32 or fp64; the noise is torch's CPU generator (as in the reference).
+"""
+import math
+import os
+import time
+
+import torch
+
+
+def host_cores():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota when one is set
+    (a GPU box's share of a large host is a quota, not a smaller affinity mask)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or platform.machine()
+
+
+def _u_grad(net, s, X):
+    sx = torch.cat([s, X], -1).requires_grad_(True)
+    with torch.enable_grad():
+        u = net(sx)
+        (g,) = torch.autograd.grad(u.sum(), sx, allow_unused=True) if u.requires_grad else (None,)
+    if g is None:  # ZeroSolution: grad u := 0 (utils.py:80-94)
+        g = torch.zeros_like(sx)
+    return u.detach(), g[:, 1:]
+
+
+def labels_reference_algorithm(eq, net, tx, M, gen, noise=None):
+    """(n, 1+nx) labels for points tx (n, 1+nx), M paths each, in tx's dtype.  `noise` = (xi (R, nx),
+    U (R, 1), zeta (R, nx)), R = n M, replaces the three path draws (tests pin the algorithm
+    against the reference's golden outputs this way)."""
+    n, nx = tx.shape[0], eq.nx
+    dt = tx.dtype
+    T = float(eq.T)
+    a = math.sqrt(float(eq.alpha))
+    t = tx[:, :1].repeat_interleave(M, 0)
+    x = tx[:, 1:].repeat_interleave(M, 0)
+    ones = torch.ones(n * M, 1, dtype=dt)
+    # terminal estimator (data.py:899-926)
+    xi = torch.randn(n * M, nx, generator=gen, dtype=dt) if noise is None else noise[0]
+    tau = torch.sqrt(T - t)
+    gx = eq.g(tx[:, 1:])
+    c = (eq.g(x + tau * a * xi) - gx.repeat_interleave(M, 0)) * torch.cat([ones, xi / tau / a], -1)
+    y = c.view(n, M, 1 + nx).mean(1)
+    y[:, :1] += gx
+    # integral estimator (data.py:471-527, generate_sx_for_integral :350-366)
+    U = torch.rand(n * M, 1, generator=gen, dtype=dt) if noise is None else noise[1]
+    s = U * (T - t) + t
+    zeta = torch.randn(n * M, nx, generator=gen, dtype=dt) if noise is None else noise[2]
+    sig = torch.sqrt(s - t)
+    Xs = x + sig * a * zeta
+    u, ux = _u_grad(net, s, Xs)
+    f = eq.ff(s, Xs, u, ux)
+    ub, uxb = _u_grad(net, tx[:, :1], tx[:, 1:])  # baseline once per point (get_f baseline_repeat)
+    fb = eq.ff(tx[:, :1], tx[:, 1:], ub, uxb).repeat_interleave(M, 0)
+    c = (T - t) * (f - fb) * torch.cat([ones, zeta / sig / a], -1)
+    c[:, :1] += fb * (T - t)
+    return y + c.view(n, M, 1 + nx).mean(1)
+
+
+def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, points_per_call=4, threads=None):
+    """path-labels/s of labels_reference_algorithm on `threads` host threads for ~target_s seconds."""
+    threads = threads or host_cores()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    net = net.to(dtype)
+    gen = torch.Generator().manual_seed(0)
+    done = calls = 0
+    try:
+        labels_reference_algorithm(eq, net, sample_points(points_per_call, 0).to(dtype), M, gen)  # warm-up
+        t0 = time.perf_counter()
+        while True:
+            tx = sample_points(points_per_call, calls * points_per_call).to(dtype)
+            y = labels_reference_algorithm(eq, net, tx, M, gen)
+            assert torch.isfinite(y).all()
+            done += points_per_call * M
+            calls += 1
+            dt = time.perf_counter() - t0
+            if dt >= target_s:
+                break
+    finally:
+        torch.set_num_threads(prev)
+    return done / dt, calls * points_per_call, dt, threads

@@ -1,0 +1,78 @@
+"""Full BASELINE sizes for the PISGradNet and SDGD workloads (the Burgers ones are in
+test_gpu_parity.py): HJB configs[2] (64 points x 4096 paths, K = 50, PISGradNet 4x512 — one
+262,144-row chunk through the GEMM pipeline) and GBM configs[4] (64 points x 1024 paths, K = 50,
+SDGD v = 100).  Checks: bitwise-reproducible moments, 2 / 4 / 8 MC shards reduced with
+dpi_moments_reduce equal to the single call bit for bit, and the first and last point within the
+north star's rel-L2 1e-4 of the fp64 oracle on the same counters."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    import deeppicarditeration_amd._lib as L
+    L.load()
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _check(gen, oeq, onet, n, M, K, v=0):
+    from deeppicarditeration_amd import _lib as L
+    from oracle import dpi_oracle as O
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    ws = gen.point_baseline(tx)
+    full = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+    again = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+    assert torch.equal(full, again)
+    for G in (2, 4, 8):
+        parts = torch.stack([gen.label_moments(tx, 0, M, r * M // G, (r + 1) * M // G, L.DPI_BOTH, ws)
+                             for r in range(G)]).contiguous()
+        assert torch.equal(gen.moments_reduce(parts), full), G
+    y = gen.finalize(full, M, L.DPI_BOTH, ws).cpu().double().numpy()
+    assert np.isfinite(y).all()
+    txh = tx.cpu().double().numpy()
+    for i in (0, n - 1):
+        ref = O.labels_grad(oeq, onet, txh[i:i + 1], M, K, 1, 1, i, v=v, m_chunk=512)
+        ev, eg = _rel(y[i:i + 1, :1], ref[:, :1]), _rel(y[i:i + 1, 1:], ref[:, 1:])
+        print(f"point {i}: value {ev:.2e} grad {eg:.2e}")
+        assert ev < TOL and eg < TOL, (i, ev, eg)
+
+
+def test_hjb_config2_full_size():
+    import deeppicarditeration_amd as dpi
+    from oracle import dpi_oracle as O
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(0)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    n, M, K = 64, 4096, 50
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    _check(gen, oeq, onet, n, M, K)
+
+
+def test_gbm_config4_full_size():
+    import deeppicarditeration_amd as dpi
+    from oracle import dpi_oracle as O
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    torch.manual_seed(3)
+    net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+    n, M, K, v = 64, 1024, 50, 100
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": v}})
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
+                 ["ELU"] * 3)
+    _check(gen, O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy()), onet, n, M, K, v=v)

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU call of a round: GPU tests, bench lines for every workload, kernel traces (one stream for
+# HJB), the counter list and the VALU / HBM PMC passes of the Burgers bench.
+# usage: tools/gpu_round.sh <tag> [tests|bench|trace|pmc ...]   outputs under gpurun_out/<tag>/
+set -e
+tag=${1:-r02}; shift || true
+what=${*:-tests bench trace pmc}
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+run() { tools/gpu_check.sh "$@"; }
+for w in $what; do
+  case $w in
+  tests)
+    run 900 $out/gpu_tests.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+  bench)
+    run 300 $out/bench_burgers.log python bench.py
+    run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
+    run 300 $out/bench_gbm.log python bench.py --workload gbm --steps 20 --warmup 3
+    run 300 $out/bench_gbm_hess.log python bench.py --workload gbm_hess --steps 10 --warmup 2 ;;
+  trace)
+    for wl in burgers gbm gbm_hess; do
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_$wl -o trace --output-format csv -- \
+        python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_$wl.log 2>&1
+    done
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
+      python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline --no-prepare > $out/trace_hjb_onestream.log 2>&1 ;;
+  counters)
+    timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
+  pmc)
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+      --kernel-include-regex k_paths -d $out/pmc_valu -o pmc --output-format csv -- \
+      python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu.log 2>&1
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_reduce" -d $out/pmc_burgers_$c -o pmc \
+        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_burgers_$c.log 2>&1
+    done ;;
+  esac
+done
