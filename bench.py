@@ -32,6 +32,8 @@ PEAK_F16_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense MFMA peak
 # fp16-split MFMA (include/dpi.h DPI_GEMM_F16X3, the default): one fp32 product = 3 f16 products
 PEAK_SPLIT_TFLOPS = PEAK_F16_TFLOPS / 3.0
 PEAK_HBM_GBS = 8000.0
+N_SIMD = 1024          # 256 CUs x 4 SIMDs
+PEAK_CLOCK_GHZ = 2.4   # MI355X peak engine clock (MI355X_MICROARCH.md)
 # workloads = BASELINE.json configs; FLOP per path-label from SURVEY.md §8(d), except GBM, whose
 # kernel runs a cheaper algorithm than §8(d) assumes (adjoint + first-order tangents instead of
 # second-order forward mode): there the FLOPs it executes are counted.
@@ -344,6 +346,25 @@ def main():
         else:
             peak = PEAK_FP32_TFLOPS
             peak_basis = "fp32 MFMA (v_mfma_f32_16x16x4_f32) = fp32 vector peak"
+        mfma = {"achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                "peak_basis": peak_basis, "flop_per_path_label": FLOP_PER_PATH_LABEL}
+        # the fused kernels are VALU-issue bound (Philox4x32-10 + Box-Muller of the 2 K nx normals per
+        # path-label): their roofline is the VALU issue of the 1024 SIMDs at the 2.4 GHz
+        # peak clock.  Busy cycles per launch come from the PMC pass of this command
+        # (profiles/valu_<workload>.json; the kernel's instruction stream is fixed, so they are a constant
+        # of the launch); the launch time is measured live.
+        valu = None
+        vf = ROOT / "profiles" / f"valu_{args.workload}.json"
+        if vf.exists() and not wl.get("pis"):
+            kern = json.loads(vf.read_text())["kernels"]
+            # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD>: the network launch, not the u = 0 twin
+            net_k = [v for k, v in kern.items() if k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
+            busy = max(net_k, key=lambda v: v["dispatches"])["valu_busy_cycles_per_simd"]
+            valu = {"achieved": busy * N_SIMD / (k_ms * 1e-3) / 1e12, "peak": N_SIMD * PEAK_CLOCK_GHZ * 1e9 / 1e12,
+                    "unit": "T VALU-busy SIMD-cycles/s", "valu_busy_cycles_per_simd": busy,
+                    "busy_source": f"profile_derived: profiles/valu_{args.workload}.json (SQ_ACTIVE_INST_VALU x 4 / "
+                                   "1024 SIMDs per launch)"}
+            valu["frac"] = valu["achieved"] / valu["peak"]
         traffic = None
         tf = ROOT / "profiles" / f"traffic_{args.workload}.json"
         if tf.exists():
@@ -368,16 +389,18 @@ def main():
                                     else "two-phase (all-gather overlapped)" if pipelined else "one labels() call"),
                        "prewarm_steps": prewarm,
                        "rel_l2_vs_ref": parity},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                         "frac": achieved / peak, "traffic": traffic,
+            "roofline": {"bound": "valu" if valu else "mfma", **({k: valu[k] for k in ("achieved", "peak", "unit", "frac")}
+                                                                  if valu else
+                                                                  {k: mfma[k] for k in ("achieved", "peak", "unit", "frac")}),
+                         "traffic": traffic,
                          "traffic_source": (f"profile_derived: profiles/traffic_{args.workload}.json (rocprofv3 PMC "
                                             "FETCH_SIZE / WRITE_SIZE passes of this bench command, HBM bytes per "
                                             "label call)") if traffic is not None else None,
-                         "peak_basis": peak_basis, "kernel": wl["kernel"],
-                         "kernel_ms": k_ms, "flop_per_path_label": FLOP_PER_PATH_LABEL},
+                         "kernel": wl["kernel"], "kernel_ms": k_ms,
+                         "valu": valu, "mfma": mfma},
         }
         if "survey_flop" in wl:
-            out["roofline"]["survey_flop_per_path_label"] = wl["survey_flop"]
+            out["roofline"]["mfma"]["survey_flop_per_path_label"] = wl["survey_flop"]
         if floor_ms is not None:
             out["roofline"]["noise_floor"] = {
                 "what": "same launch with u = 0 (ZeroSolution): Philox4x32-10 + Box-Muller + K-step EM only, the "

@@ -1779,9 +1779,11 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
 
   // ---------------- phase 3: per-path contributions -> per-block partial slab
   const float bp = sh.bsh[lane];
-  // partial slab layout [point][2F][block]: the reduce kernel reads each column's blocks contiguously
-  float* out = a.partial + (size_t)i * 2 * F * a.nbp + blk;
-  const int nbs = a.nbp;
+  // partial slab layout [point][block][slab_row(F)]: this workgroup's 2F sums are one contiguous,
+  // 128-B aligned row, so every HBM line of the slab is written from a single XCD (a column-major
+  // [point][2F][block] slab had the blocks of one line written from all eight XCDs' L2s, each
+  // writing its dirty bytes back separately: 7.8x the slab in WRITE_SIZE)
+  float* out = a.partial + ((size_t)i * a.nbp + blk) * slab_row(F);
   // per-block sums of c and c^2 for this wave's columns: 2 per owned dim (d = 4 (wv + 4c) + q,
   // column 8c + 2q + {0: sum, 1: sum of squares}) and, on wave 0, the value column (56, 57)
   const float aY = ap * yT, bY = bp * yI;
@@ -1816,9 +1818,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
     const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
     const int d = 4 * (wv + 4 * c) + q;
     if (lane < 56) {
-      if (wv + 4 * c < nb && d < nx) out[(size_t)(sq * F + 1 + d) * nbs] = tot;
+      if (wv + 4 * c < nb && d < nx) out[sq * F + 1 + d] = tot;
     } else if (wv == 0 && lane < 58) {
-      out[(size_t)(sq * F) * nbs] = tot;
+      out[sq * F] = tot;
     }
   }
   if (wv + 28 < nb) {  // nx > 112: the eighth dim-block of this wave, one column at a time
@@ -1829,8 +1831,8 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
         const float v = fmaf(aY, ST[7][q], bY * sh.S[d * SS + lane]);
         const float s1 = wave_sum(v), s2 = wave_sum(v * v);
         if (lane == 0) {
-          out[(size_t)(1 + d) * nbs] = s1;
-          out[(size_t)(F + 1 + d) * nbs] = s2;
+          out[1 + d] = s1;
+          out[F + 1 + d] = s2;
         }
       }
     }

@@ -11,6 +11,11 @@
 
 namespace dpi {
 
+// Row length (floats) of the per-(point, 64-path block) partial slab: the 2F column sums (c, c^2)
+// rounded up to 128 B, so the rows of different workgroups never share an HBM line.
+__host__ __device__ constexpr int slab_row(int F) { return (2 * F + 31) & ~31; }
+
+
 constexpr int NSG = 8;  // max per-path g statistics (OU mixture components)
 
 struct EqDev {

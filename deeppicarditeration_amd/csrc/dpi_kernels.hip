@@ -52,26 +52,28 @@ __device__ __forceinline__ float tree_sum(const float* __restrict__ p, int cnt, 
   return s;
 }
 
-// partial [n][2F][nbp] -> moments [n][2F] (and, if y != nullptr, the finalized labels).
+// partial [n][nbp][slab_row(F)] -> moments [n][2F] (and, if y != nullptr, the finalized labels).
 // torch.clip of the reference (data.py:222): NaN stays NaN (fmaxf alone would return -bound).
 __device__ __forceinline__ float clip_label(float v, float bound) {
   return v != v ? v : fminf(fmaxf(v, -bound), bound);
 }
 
-__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
-                                                float* __restrict__ moments, const float* __restrict__ gx,
-                                                float invM, int add_g, float bound, float* __restrict__ y,
-                                                int ystride) {
-  const int i = blockIdx.x;
-  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (c >= 2 * F) return;
-  const float s = tree_sum(partial + ((size_t)i * 2 * F + c) * nbp, nbp, 1);
-  if ((threadIdx.x & 63) == 0) {
-    moments[(size_t)i * 2 * F + c] = s;
-    if (y && c < F) {
-      float v = s * invM;
-      if (c == 0 && add_g) v += gx[i];
-      y[(size_t)i * ystride + c] = clip_label(v, bound);
+__global__ __launch_bounds__(1024) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
+                                                 float* __restrict__ moments, const float* __restrict__ gx,
+                                                 float invM, int add_g, float bound, float* __restrict__ y,
+                                                 int ystride) {
+  // one workgroup per point (its slab is read by one XCD), a wave per column, 16 columns at a time
+  const int i = blockIdx.x, R = slab_row(F);
+  const float* slab = partial + (size_t)i * nbp * R;
+  for (int c = threadIdx.x >> 6; c < 2 * F; c += 16) {
+    const float s = tree_sum(slab + c, nbp, (size_t)R);
+    if ((threadIdx.x & 63) == 0) {
+      moments[(size_t)i * 2 * F + c] = s;
+      if (y && c < F) {
+        float v = s * invM;
+        if (c == 0 && add_g) v += gx[i];
+        y[(size_t)i * ystride + c] = clip_label(v, bound);
+      }
     }
   }
 }
@@ -737,7 +739,7 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
     rows_bytes = al256((size_t)w.rows_cap * stride * 4);
   }
   w.partial = w.rows + rows_bytes;
-  w.total = w.partial + (size_t)n * nbp * 2 * F * 4;
+  w.total = w.partial + (size_t)n * nbp * slab_row(F) * 4;
   return w;
 }
 
@@ -1099,7 +1101,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
       return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
   }
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
+  hipLaunchKernelGGL(k_reduce, dim3(n), dim3(1024), 0, st, partial, n, F, nbp, moments,
                      (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1225,7 +1227,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   if (!dispatch_any(p, net, q))
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
+  hipLaunchKernelGGL(k_reduce, dim3(n), dim3(1024), 0, st, a.partial, n, F, nbp, moments, a.gx,
                      1.0f / (float)M, 1, bound, y, F + C);
   hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
                      1.0f / (float)M, bound, y, F + C, F);

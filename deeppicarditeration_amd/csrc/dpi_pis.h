@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   }
   __syncthreads();
   // fixed-order (pairwise) sum over the 64 paths of each column
-  float* out = partial + (size_t)i * 2 * F * nbp + b;
+  float* out = partial + ((size_t)i * nbp + b) * slab_row(F);  // [point][block][slab_row(F)]
   for (int c = tid; c < 2 * F; c += NTH) {
     const int mom = c >= F, col = c - mom * F;
     float v[P];
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
     for (int w = 1; w < P; w <<= 1)
 #pragma unroll
       for (int k = 0; k < P; k += 2 * w) v[k] += v[k + w];
-    out[(size_t)c * nbp] = v[0];
+    out[c] = v[0];
   }
 }
 

@@ -98,8 +98,8 @@ def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, poi
         t0 = time.perf_counter()
         while True:
             tx = sample_points(points_per_call, calls * points_per_call).to(dtype)
-            y = labels_reference_algorithm(eq, net, tx, M, gen)
-            assert torch.isfinite(y).all()
+            # (no finiteness check: in fp32 the reference's s - t rounds to 0 for tiny U, giving inf)
+            labels_reference_algorithm(eq, net, tx, M, gen)
             done += points_per_call * M
             calls += 1
             dt = time.perf_counter() - t0

@@ -28,12 +28,16 @@ for w in $what; do
   counters)
     timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
   pmc)
-    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-      --kernel-include-regex k_paths -d $out/pmc_valu -o pmc --output-format csv -- \
-      python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu.log 2>&1
-    for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_reduce" -d $out/pmc_burgers_$c -o pmc \
-        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_burgers_$c.log 2>&1
+    for wl in burgers gbm gbm_hess; do
+      timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+        --kernel-include-regex k_paths -d $out/pmc_valu_$wl -o pmc --output-format csv -- \
+        python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu_$wl.log 2>&1
+    done
+    for wl in burgers hjb gbm gbm_hess; do
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm|k_reduce" -d $out/pmc_${wl}_$c -o pmc \
+          --output-format csv -- python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_${wl}_$c.log 2>&1
+      done
     done ;;
   esac
 done

@@ -56,3 +56,36 @@ for wl, anchor in ANCHOR.items():
          "source": f"profiles/{tag}_pmc_{wl}_FETCH_SIZE.json, profiles/{tag}_pmc_{wl}_WRITE_SIZE.json"}
     (dst / f"traffic_{wl}.json").write_text(json.dumps(t, indent=1))
     print(json.dumps(t, indent=1))
+# VALU issue per launch (pmc_valu_<wl>: SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU, SQ_INSTS_MFMA, SQ_INSTS_SALU,
+# SQ_BUSY_CYCLES, SQ_WAVE_CYCLES, GRBM_GUI_ACTIVE on k_paths): per kernel variant (the network launch
+# and the bench's u = 0 noise-floor launch), averaged over dispatches.  SQ_ACTIVE_INST_VALU is in
+# quad-cycles summed over all SIMDs (1024); GRBM_GUI_ACTIVE is summed over the 8 XCDs.
+N_SIMD, N_XCD = 1024, 8
+for wl in ("burgers", "gbm", "gbm_hess"):
+    f = src / f"pmc_valu_{wl}" / "pmc_counter_collection.csv"
+    if not f.exists() and wl == "burgers":
+        f = src / "pmc_valu" / "pmc_counter_collection.csv"
+    if not f.exists():
+        continue
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        per[(name, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    kinds = collections.defaultdict(list)
+    for (name, _), c in per.items():
+        kinds[name].append(c)
+    out = {"command": f"rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES "
+                      f"SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex k_paths -- python bench.py --workload {wl} "
+                      "--steps 10 --warmup 2 --no-cpu-baseline",
+           "units": "per launch; valu_busy_cycles_per_simd = SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs; kernel_cycles = "
+                    "GRBM_GUI_ACTIVE / 8 XCDs; valu_busy = their ratio (the rocprofv3 VALUBusy expression)",
+           "kernels": {}}
+    for name, lst in kinds.items():
+        avg = {k: sum(c[k] for c in lst) / len(lst) for k in lst[0]}
+        busy = avg["SQ_ACTIVE_INST_VALU"] * 4 / N_SIMD
+        cyc = avg["GRBM_GUI_ACTIVE"] / N_XCD
+        out["kernels"][name] = {"dispatches": len(lst), **{k: round(v) for k, v in avg.items()},
+                                "valu_busy_cycles_per_simd": busy, "kernel_cycles": cyc, "valu_busy": busy / cyc,
+                                "valu_insts_per_simd": avg["SQ_INSTS_VALU"] / N_SIMD}
+    (dst / f"valu_{wl}.json").write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
