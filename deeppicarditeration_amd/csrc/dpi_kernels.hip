@@ -58,22 +58,22 @@ __device__ __forceinline__ float clip_label(float v, float bound) {
   return v != v ? v : fminf(fmaxf(v, -bound), bound);
 }
 
-__global__ __launch_bounds__(1024) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
-                                                 float* __restrict__ moments, const float* __restrict__ gx,
-                                                 float invM, int add_g, float bound, float* __restrict__ y,
-                                                 int ystride) {
-  // one workgroup per point (its slab is read by one XCD), a wave per column, 16 columns at a time
+__global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
+                                                float* __restrict__ moments, const float* __restrict__ gx,
+                                                float invM, int add_g, float bound, float* __restrict__ y,
+                                                int ystride) {
+  // a wave per (point, column): reading the slab's lines from several XCDs costs only duplicate
+  // fetches of a 0.9 MB slab, while one workgroup per point serialised the columns (14 vs 4.4 us)
   const int i = blockIdx.x, R = slab_row(F);
-  const float* slab = partial + (size_t)i * nbp * R;
-  for (int c = threadIdx.x >> 6; c < 2 * F; c += 16) {
-    const float s = tree_sum(slab + c, nbp, (size_t)R);
-    if ((threadIdx.x & 63) == 0) {
-      moments[(size_t)i * 2 * F + c] = s;
-      if (y && c < F) {
-        float v = s * invM;
-        if (c == 0 && add_g) v += gx[i];
-        y[(size_t)i * ystride + c] = clip_label(v, bound);
-      }
+  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (c >= 2 * F) return;
+  const float s = tree_sum(partial + (size_t)i * nbp * R + c, nbp, (size_t)R);
+  if ((threadIdx.x & 63) == 0) {
+    moments[(size_t)i * 2 * F + c] = s;
+    if (y && c < F) {
+      float v = s * invM;
+      if (c == 0 && add_g) v += gx[i];
+      y[(size_t)i * ystride + c] = clip_label(v, bound);
     }
   }
 }
@@ -732,9 +732,8 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   w.rows_cap = 0;
   size_t rows_bytes = 0;
   if (net && net->d.kind == 2) {
-    const size_t need = std::max((size_t)n, (size_t)n * nbp * P);
-    w.rows_cap = (int)std::min(need, (size_t)pis_chunk_wg() * P);
-    w.rows_cap = std::max(w.rows_cap, (int)std::min((size_t)n, (size_t)pis_chunk_wg() * P));
+    // a chunk of path rows plus the n per-point baseline rows, which ride in the first chunk's chain
+    w.rows_cap = (int)std::min((size_t)n * nbp * P, (size_t)pis_chunk_wg() * P) + n;
     const int stride = std::max(pis_rows_layout(net->pis, false).stride, pis_rows_layout(net->pis, true).stride);
     rows_bytes = al256((size_t)w.rows_cap * stride * 4);
   }
@@ -956,29 +955,11 @@ static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, cons
                         hipStream_t st) {
   int rc = pis_check(p);
   if (rc) return rc;
-  float *gx = (float*)(b + w.gx), *fb = (float*)(b + w.fb), *rows = (float*)(b + w.rows);
-  // g(x) (k_baseline's zero-net instance also writes a placeholder f_b, overwritten below)
-  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTHB), 0, st, p->e, net->d, tx, n, gx, fb,
-                     (float*)(b + w.bx), (float*)(b + w.hb));
-  const int F = 1 + p->e.nx;
-  const bool x3 = pis_x3(net->pis);
-  const PisRows L = pis_rows_layout(net->pis, x3);
-  for (int i0 = 0; i0 < n; i0 += w.rows_cap) {
-    const int R = std::min(w.rows_cap, n - i0);
-    if (x3) {
-      hipLaunchKernelGGL(k_pis_points<true>, dim3(R), dim3(64), 0, st, p->e.nx, net->pis, tx + (size_t)i0 * F, R, rows,
-                         L);
-      const PisRows Lc = pis_chain_x3(net->pis, rows, R, st);
-      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, true>), dim3((R + 15) / 16), dim3(64), 0, st, p->e, net->pis,
-                         rows, Lc, R, fb + i0);
-    } else {
-      hipLaunchKernelGGL(k_pis_points<false>, dim3(R), dim3(64), 0, st, p->e.nx, net->pis, tx + (size_t)i0 * F, R,
-                         rows, L);
-      const PisRows Lc = pis_chain(net->pis, rows, R, st);
-      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, false>), dim3((R + 15) / 16), dim3(64), 0, st, p->e, net->pis,
-                         rows, Lc, R, fb + i0);
-    }
-  }
+  // g(x) only (k_baseline's zero-net instance; its f_b placeholder is overwritten by pis_paths): the
+  // per-point f_b = f(t, x, u, grad u) needs the whole PISGradNet chain, so its n rows ride in the
+  // first path chunk's chain (pis_paths) instead of a separate 15-launch chain over n rows
+  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTHB), 0, st, p->e, net->d, tx, n,
+                     (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -988,16 +969,20 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
   int rc = pis_check(p);
   if (rc) return rc;
   float* rows = (float*)(b + w.rows);
+  float* fb = (float*)(b + w.fb);
   const bool x3 = pis_x3(net->pis);
   const PisRows L = pis_rows_layout(net->pis, x3);
-  const int G = n * a.nbp, GC = std::max(1, w.rows_cap / P);
+  const int G = n * a.nbp, GC = std::max(1, (w.rows_cap - n) / P);
   const float dt = a.td_dt;
   // TD estimators: a terminal stage (rollout to t_next, forward chain, a_p = u(t_next, X) - g(x))
   // before the integral stage; the plain estimators run both paths in one rollout.
+  // The first chunk's integral chain also carries the n baseline rows (t_i, x_i) after its g P path
+  // rows: f_b comes out of the same GEMM launches (row results do not depend on where a row sits in
+  // the chunk) and lands before k_pis_final reads it.
   auto chunk = [&](auto x3c, int g0, int g) {
     constexpr bool X3 = decltype(x3c)::value;
-    auto chain = [&](bool vjp) {
-      return X3 ? pis_chain_x3(net->pis, rows, g * P, st, vjp) : pis_chain(net->pis, rows, g * P, st, vjp);
+    auto chain = [&](bool vjp, int R) {
+      return X3 ? pis_chain_x3(net->pis, rows, R, st, vjp) : pis_chain(net->pis, rows, R, st, vjp);
     };
     auto rollout = [&](int stage) {
       hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp,
@@ -1007,7 +992,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     if (dt > 0.f) {
       rollout(PIS_TD_TERM);
       if (a.flags & DPI_TERMINAL) {
-        const PisRows Lt = chain(false);
+        const PisRows Lt = chain(false, g * P);
         hipLaunchKernelGGL((k_pis_tvalue<DPI_EQ_OU, X3>), dim3(g), dim3(256), 0, st, p->e, net->pis, tx, g0, a.nbp,
                            a.gx, rows, Lt, g * P, dt);
       }
@@ -1015,9 +1000,16 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     } else {
       rollout(PIS_BOTH);
     }
-    const PisRows Lc = chain(true);
+    const bool base = g0 == 0;
+    float* brows = rows + (size_t)g * P * L.stride;
+    if (base)
+      hipLaunchKernelGGL(k_pis_points<X3>, dim3(n), dim3(64), 0, st, p->e.nx, net->pis, tx, n, brows, L);
+    const PisRows Lc = chain(true, g * P + (base ? n : 0));
+    if (base)
+      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 15) / 16), dim3(64), 0, st, p->e, net->pis,
+                         brows, Lc, n, fb);
     hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
-                       a.flags, a.fb, rows, Lc, a.partial, dt);
+                       a.flags, fb, rows, Lc, a.partial, dt);
   };
   for (int g0 = 0; g0 < G; g0 += GC) {
     const int g = std::min(GC, G - g0);
@@ -1101,7 +1093,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
       return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
   }
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_reduce, dim3(n), dim3(1024), 0, st, partial, n, F, nbp, moments,
+  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
                      (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1227,7 +1219,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   if (!dispatch_any(p, net, q))
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_reduce, dim3(n), dim3(1024), 0, st, a.partial, n, F, nbp, moments, a.gx,
+  hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
                      1.0f / (float)M, 1, bound, y, F + C);
   hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
                      1.0f / (float)M, bound, y, F + C, F);
