@@ -11,12 +11,12 @@ from pathlib import Path
 
 src, tag = Path(sys.argv[1]), sys.argv[2]
 dst = Path(__file__).resolve().parents[1] / "profiles"
-for wl in ("burgers", "hjb", "gbm", "gbm_hess"):
+for wl in ("burgers", "hjb", "gbm", "gbm_hess", "hjb_onestream"):
     f = src / f"trace_{wl}" / "trace_kernel_stats.csv"
     if f.exists():
         rows = list(csv.DictReader(open(f)))
-        out = {"command": f"rocprofv3 --kernel-trace --stats -- python bench.py --workload {wl} --steps 10 --warmup 2 "
-                          "--no-cpu-baseline",
+        out = {"command": f"rocprofv3 --kernel-trace --stats -- python bench.py --workload {wl.split('_one')[0]} "
+                          f"--steps 10 --warmup 2 --no-cpu-baseline{' --no-prepare' if 'onestream' in wl else ''}",
                "kernels": [{"name": r["Name"][:160], "calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
                             "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3,
                             "pct": float(r["Percentage"])} for r in rows]}
