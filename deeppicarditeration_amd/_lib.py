@@ -16,6 +16,7 @@ DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
 DPI_ACT_ELU = 1
 DPI_TERMINAL, DPI_INTEGRAL, DPI_BOTH = 1, 2, 3
+DPI_PREPARED = 4  # dpi_label_moments: dpi_label_prepare already ran with the same arguments
 DPI_PATH_BLOCK = 64
 DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
 
@@ -46,6 +47,8 @@ SIGNATURES = {
     "dpi_point_baseline": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "dpi_label_moments": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
                                   c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dpi_label_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
+                                  c_int, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "dpi_moments_reduce": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "dpi_label_finalize": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_size_t,
                                    c_void_p]),

@@ -217,9 +217,15 @@ __device__ __forceinline__ int x3_swz(int r) { return ((r >> 1) & 7) ^ ((((r + 4
 
 constexpr int X3_BM = 256, X3_STAGES = 3, X3_THREADS = 512;
 
-template <int EPI, int NT>
+// Two-source K: chunks c >= nk1 of the X operand come from X2 (chunk c - nk1, row stride ldx2), so
+// [X | X2] . W^T runs as one GEMM (nk1 = Kp / 32 for a single source).
+// VAR (schedule experiments, tools/ubench_x3.hip; 0 = product): bit 0 s_setprio 1 for waves 4-7,
+// bit 1 fragment reads front-loaded into the first 2/3 of the MFMAs, bit 2 the DMA issue interleaved
+// with the first MFMAs.
+template <int EPI, int NT, int VAR = 0>
 __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
                                                            float wscale, const float* __restrict__ X, int ldx,
+                                                           const float* __restrict__ X2, int ldx2, int nk1,
                                                            float* __restrict__ OUT, int ldc,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ AUX, int ldaux) {
@@ -240,11 +246,15 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
   const int m0 = mt * BM, n0 = nt * BN;
   const int nk = Kp >> 5;
   const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
+  const uint32_t* X2w = reinterpret_cast<const uint32_t*>(X2);
 
   // LDS-DMA of chunk c into ring slot `slot`: wave-instruction w fills rows 8w..8w+7 (128 B each)
   // lane-linearly; lane i fetches the granule that belongs at position i & 7 of its row.
   auto issue = [&](int c, int slot) {
     uint32_t* dst = sm + slot * STAGE;
+    const bool one = c < nk1;  // wave-uniform source select
+    const uint32_t* xb = one ? Xw + 32 * c : X2w + 32 * (c - nk1);
+    const int ld = one ? ldx : ldx2;
 #pragma unroll
     for (int k = 0; k < PER_WAVE; ++k) {
       const int w = k * NWAVE + wv;
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
       if (r < BN)
         src = W + (size_t)(n0 + r) * Kp + 32 * c + 4 * g;
       else
-        src = Xw + (size_t)min(m0 + r - BN, M - 1) * ldx + 32 * c + 4 * g;
+        src = xb + (size_t)min(m0 + r - BN, M - 1) * ld + 4 * g;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
     }
@@ -306,12 +316,30 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
     issue(min(u + 3, nk - 1), u % X3_STAGES);
     load((u + 1) % X3_STAGES, std::integral_constant<int, F ^ 1>{});
     mma(Fc);
+    constexpr int NRD = 2 * (NT + 4), NMF = 3 * NT * 4;  // ds_reads and MFMAs per chunk
+    if constexpr (VAR & 4) {  // the DMA wave-instructions between the first MFMAs
 #pragma unroll
-    for (int i = 0; i < 2 * (NT + 4); ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
-      __builtin_amdgcn_sched_group_barrier(0x008, 3 * NT * 4 / (2 * (NT + 4)), 0);  // then MFMAs
+      for (int i = 0; i < PER_WAVE; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM read (LDS-DMA)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
+    if constexpr (VAR & 2) {  // all reads within the first 2/3 of the MFMAs, then the rest of the MFMAs
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, (2 * NMF / 3 - ((VAR & 4) ? PER_WAVE : 0)) / NRD, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NRD; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 ds_read
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF / NRD, 0);  // then MFMAs
+      }
     }
   };
+  if constexpr (VAR & 1)
+    if (wv >= 4) __builtin_amdgcn_s_setprio(1);
   // prologue: chunks 0, 1, 2 (clamped) in flight; publish chunk 0 and read it
   issue(0, 0);
   issue(min(1, nk - 1), 1);
@@ -372,5 +400,6 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
     }
   }
 }
+
 
 }  // namespace dpi

@@ -554,8 +554,8 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
   const int INP = (C + nx + 31) & ~31, NXK = (nx + 31) & ~31, NOP = r64(nx);
   int hp[4];
   for (int l = 0; l < L; ++l) hp[l] = r64(hidden[l]);
-  size_t s_te0, s_te2, s_sn0, s_sn[4] = {0}, s_nn[5] = {0}, s_nnT[5] = {0}, s_nnbP[5] = {0};
-  float w_te0 = 1.f, w_te2 = 1.f, w_sn0 = 1.f, w_sn[4] = {1.f, 1.f, 1.f, 1.f}, w_nn[5], w_nnT[5];
+  size_t s_te0, s_te2, s_sn0, s_sn[4] = {0}, s_nn[5] = {0}, s_nnT[5] = {0}, s_nnbP[5] = {0}, s_gxno = 0;
+  float w_te0 = 1.f, w_te2 = 1.f, w_sn0 = 1.f, w_sn[4] = {1.f, 1.f, 1.f, 1.f}, w_nn[5], w_nnT[5], w_gxno = 1.f;
   {
     auto align = [&]() { blob.resize((blob.size() + 31) & ~size_t(31), 0.f); };
     auto packm = [&](const float* src, int rows, int cols, int Np, int Kp, bool trans, float* ws) {
@@ -583,6 +583,17 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
       s_nnT[0] = pack_split_x3(blob, NOP, hp[0], [&](int d, int h) {
         return (d < nx && h < h0) ? w0[(size_t)h * in0 + C + d] : 0.f;
       }, &w_nnT[0]);
+    }
+    {  // [nnT[0] | nn[L]]: row d, columns h < hp0 from nn[0][h][64 + d], then nn[L][d][k]
+      align();
+      const float *w0 = nnw[0], *wl = nnw[L];
+      const int in0 = ins[0], h0 = hidden[0], inl = ins[L];
+      s_gxno = pack_split_x3(blob, NOP, hp[0] + hp[L - 1], [&](int d, int k) {
+        if (d >= nx) return 0.f;
+        if (k < hp[0]) return k < h0 ? w0[(size_t)k * in0 + C + d] : 0.f;
+        k -= hp[0];
+        return k < inl ? wl[(size_t)d * inl + k] : 0.f;
+      }, &w_gxno);
     }
     for (int l = 0; l <= L; ++l) {
       const int o = l < L ? hidden[l] : nx, op = l < L ? hp[l] : NOP;
@@ -634,6 +645,8 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
     pd.sn0S = u32(s_sn0);
     pd.te0W = w_te0, pd.te2W = w_te2, pd.sn0W = w_sn0;
     for (int j = 0; j < nsm; ++j) pd.snS[j] = u32(s_sn[j]), pd.snW[j] = w_sn[j];
+    pd.gxnoS = u32(s_gxno);
+    pd.gxnoW = w_gxno;
     for (int l = 0; l <= L; ++l) {
       pd.nnS[l] = u32(s_nn[l]);
       pd.nnTS[l] = u32(s_nnT[l]);
@@ -696,8 +709,8 @@ static PisRows pis_rows_layout(const NetPisDev& pd, bool x3) {
   o += rw(pd.nx);
   L.ST = o;
   o += rw(pd.nx);
-  L.SC = o;
-  o += rw(4);
+  L.SC = o;  // s, cI, a_p, s - t, [split: network time input, smooth]
+  o += rw(8);
   L.stride = o;
   return L;
 }
@@ -780,27 +793,29 @@ static void gemm(int epi, int M, int N, int K, const float* A, int lda, const fl
 // Split-storage GEMM: OUT (M x Np) = epi(X (M x Kp) W^T), all split (Np, Kp multiples of 32).
 template <int NT>
 static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
-                       float* OUT, int ldc, const float* bias, const float* aux, int ldaux, hipStream_t st) {
-  const int nnt = Np / (32 * NT), nmt = (M + X3_BM - 1) / X3_BM;
+                       const float* X2, int ldx2, int k1, float* OUT, int ldc, const float* bias, const float* aux,
+                       int ldaux, hipStream_t st) {
+  const int nnt = Np / (32 * NT), nmt = (M + X3_BM - 1) / X3_BM, nk1 = k1 / 32;
   dim3 grid(nnt * nmt), block(X3_THREADS);
   if (epi == EPI_BIAS)
-    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias, aux,
-                       ldaux);
+    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
+                       ldc, bias, aux, ldaux);
   else if (epi == EPI_BIAS_ELU)
-    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias,
-                       aux, ldaux);
+    hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1,
+                       OUT, ldc, bias, aux, ldaux);
   else
-    hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, OUT, ldc, bias, aux,
-                       ldaux);
+    hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
+                       ldc, bias, aux, ldaux);
 }
-// ws: the weight matrix's scale 2^-s (pack_split_x3)
+// ws: the weight matrix's scale 2^-s (pack_split_x3).  X2 != nullptr: K columns [k1, Kp) come from X2.
 static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx, float* OUT,
-                    int ldc, const float* bias, const float* aux, int ldaux,
-                    hipStream_t st) {  // Np % 64 == 0, Kp % 32 == 0
+                    int ldc, const float* bias, const float* aux, int ldaux, hipStream_t st,
+                    const float* X2 = nullptr, int ldx2 = 0, int k1 = 0) {  // Np % 64 == 0, Kp % 32 == 0
+  if (!X2) X2 = X, ldx2 = ldx, k1 = Kp;
   if (Np % 128 == 0)
-    gemm_x3_nt<4>(epi, M, Kp, Np, W, ws, X, ldx, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<4>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, st);
   else
-    gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, st);
 }
 
 // The PISGradNet chain of pis_chain in split storage (every width padded to 32; the x part of IN
@@ -808,14 +823,13 @@ static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws,
 static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t st, bool vjp = true) {
   PisRows L = pis_rows_layout(pd, true);
   auto r64 = [](int x) { return (x + 63) & ~63; };
-  const int ld = L.stride, C = PIS_CH, NXK = (pd.nx + 31) & ~31, NOP = r64(pd.nx);
-  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.te0S, pd.te0W, rows + L.E, ld, rows + L.T1, ld, pd.te0b, nullptr, 0, st);
-  gemm_x3(EPI_BIAS, R, C, C, pd.te2S, pd.te2W, rows + L.T1, ld, rows + L.IN, ld, pd.te2b, nullptr, 0, st);
-  int hs = L.H0, ho = L.H1;
-  gemm_x3(EPI_BIAS_ELU, R, 2 * C, C, pd.sn0S, pd.sn0W, rows + L.E, ld, rows + hs, ld, pd.sn0b, nullptr, 0, st);
-  for (int j = 0; j < pd.nsm; ++j) {
-    gemm_x3(EPI_BIAS_ELU, R, C, C, pd.snS[j], pd.snW[j], rows + hs, ld, rows + ho, ld, pd.snb[j], nullptr, 0, st);
-    std::swap(hs, ho);
+  const int ld = L.stride, NXK = (pd.nx + 31) & ~31, NOP = r64(pd.nx);
+  // t_encoder -> IN[:, 0:64] and smooth -> SC + 5 in one launch (one block per CU: 144 KB of weights in LDS)
+  if (R > 0) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = std::max(1, std::min(ncu, (R + 16 * (PT_THREADS / 64) - 1) / (16 * (PT_THREADS / 64))));
+    hipLaunchKernelGGL(k_pis_time<4>, dim3(blocks), dim3(PT_THREADS), 0, st, pd, rows, L, R);
   }
   int Kp = L.INP;
   const float* a = rows + L.IN;
@@ -824,9 +838,10 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
     a = rows + L.A[l];
     Kp = r64(pd.h[l]);
   }
-  gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
-  L.H0 = hs;
-  if (!vjp) return L;
+  if (!vjp) {  // forward only (TD terminal value): net_out
+    gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
+    return L;
+  }
   // VJP: the x part of IN starts at its chunk 2 (word 64)
   int dcur = L.D0, dnext = L.D1;
   gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], pd.nnTW[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld, nullptr,
@@ -836,8 +851,10 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
             rows + L.A[l - 1], ld, st);
     std::swap(dcur, dnext);
   }
-  gemm_x3(EPI_BIAS, R, r64(pd.h[0]), NOP, pd.nnTS[0], pd.nnTW[0], rows + dcur, ld, rows + L.GX, ld, nullptr, nullptr, 0, st);
-  L.H0 = hs;
+  // GX = J^T X + net_out = [D_0 | A_{L-1}] . [nnT[0] | nn[L]]^T + b_L: one GEMM with K = h_0 + h_{L-1}
+  // (k_pis_final and k_pis_base_final only need the sum)
+  gemm_x3(EPI_BIAS, R, r64(pd.h[0]) + Kp, NOP, pd.gxnoS, pd.gxnoW, rows + dcur, ld, rows + L.GX, ld, pd.nnbP[pd.L],
+          nullptr, 0, st, rows + L.A[pd.L - 1], ld, r64(pd.h[0]));
   return L;
 }
 
@@ -964,8 +981,10 @@ static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, cons
   return 0;
 }
 
+// prepared: dpi_label_prepare already ran the first chunk's rollout and baseline rows (same
+// arguments, same workspace); prepare_only: run just those (dpi_label_prepare).
 static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
-                     char* b, hipStream_t st) {
+                     char* b, hipStream_t st, bool prepared = false, bool prepare_only = false) {
   int rc = pis_check(p);
   if (rc) return rc;
   float* rows = (float*)(b + w.rows);
@@ -989,6 +1008,8 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
                          a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L, stage,
                          dt);
     };
+    const bool base = g0 == 0;
+    float* brows = rows + (size_t)g * P * L.stride;
     if (dt > 0.f) {
       rollout(PIS_TD_TERM);
       if (a.flags & DPI_TERMINAL) {
@@ -997,13 +1018,12 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
                            a.gx, rows, Lt, g * P, dt);
       }
       rollout(PIS_TD_INT);
-    } else {
+    } else if (!(prepared && base)) {
       rollout(PIS_BOTH);
     }
-    const bool base = g0 == 0;
-    float* brows = rows + (size_t)g * P * L.stride;
-    if (base)
+    if (base && !(prepared && dt == 0.f))
       hipLaunchKernelGGL(k_pis_points<X3>, dim3(n), dim3(64), 0, st, p->e.nx, net->pis, tx, n, brows, L);
+    if (prepare_only) return;
     const PisRows Lc = chain(true, g * P + (base ? n : 0));
     if (base)
       hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 15) / 16), dim3(64), 0, st, p->e, net->pis,
@@ -1017,6 +1037,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       chunk(std::true_type{}, g0, g);
     else
       chunk(std::false_type{}, g0, g);
+    if (prepare_only) break;  // the first chunk only
   }
   HIPCHK(hipGetLastError());
   return 0;
@@ -1044,35 +1065,37 @@ static int path_order() {
   return e ? std::atoi(e) : 0;
 }
 
-static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
-                        uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
-                        void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
+// Validates a label-moments call and fills its PathArgs (shared by dpi_label_moments and
+// dpi_label_prepare).  Returns 0, or the error; *w receives the workspace layout.
+static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                      uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, bool need_moments,
+                      const float* moments, void* ws, size_t ws_bytes, WsLayout* w, PathArgs* pa) {
   int rc = check_pair(p, net);
   if (rc) return rc;
-  if (n < 0 || (n && (!tx || !ws || !moments)) || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
-      (m_begin % P) || (m_end % P) || !(flags & DPI_BOTH) || (flags & ~DPI_BOTH) || epoch > 0xFFFFFFu)
+  if (n < 0 || (n && (!tx || !ws || (need_moments && !moments))) || K < 1 || M < 1 || m_begin < 0 || m_end > M ||
+      m_end <= m_begin || (m_begin % P) || (m_end % P) || !(flags & DPI_BOTH) || (flags & ~(DPI_BOTH | DPI_PREPARED)) ||
+      epoch > 0xFFFFFFu)
     return fail(DPI_ERR_ARG, "label_moments: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
   if (n == 0) return 0;
   const int F = 1 + p->e.nx;
   const int nbp = (m_end - m_begin) / P;
   if (nbp > 1024) return fail(DPI_ERR_ARG, "label_moments: at most 1024 x 64 paths per call");
-  const WsLayout w = ws_layout(net, n, M, F);
-  if (ws_bytes < w.total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  *w = ws_layout(net, n, M, F);
+  if (ws_bytes < w->total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
-  float* partial = (float*)(b + w.partial);
-  PathArgs a;
+  PathArgs& a = *pa;
   std::memset(&a, 0, sizeof(a));
   a.tx = tx;
-  a.gx = (const float*)(b + w.gx);
-  a.fb = (const float*)(b + w.fb);
-  a.bx = (const float*)(b + w.bx);
-  a.hb = (const float*)(b + w.hb);
-  a.partial = partial;
+  a.gx = (const float*)(b + w->gx);
+  a.fb = (const float*)(b + w->fb);
+  a.bx = (const float*)(b + w->bx);
+  a.hb = (const float*)(b + w->hb);
+  a.partial = (float*)(b + w->partial);
   a.n = n;
   a.nbp = nbp;
   a.m_begin = m_begin;
   a.K = K;
-  a.flags = flags;
+  a.flags = flags & DPI_BOTH;
   a.k0 = (uint32_t)seed;
   a.k1 = (uint32_t)(seed >> 32);
   a.c3t = DPI_TAG_TERM | (epoch << 8);
@@ -1083,9 +1106,23 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   a.order = path_order();
   a.split = mlp_split() ? 1 : 0;
   a.td_dt = p->td_dt;
+  return 0;
+}
+
+static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                        uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
+                        void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
+  WsLayout w;
+  PathArgs a;
+  int rc = label_args(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, true, moments, ws, ws_bytes,
+                      &w, &a);
+  if (rc || n == 0) return rc;
+  const int F = 1 + p->e.nx, nbp = a.nbp;
+  char* b = (char*)ws;
+  float* partial = a.partial;
   hipStream_t st = (hipStream_t)stream;
   if (net->d.kind == 2) {
-    if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st))) return rc;
+    if ((rc = pis_paths(p, net, tx, n, K, a, w, b, st, (flags & DPI_PREPARED) != 0))) return rc;
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
@@ -1097,6 +1134,17 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
                      (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,
+                      uint32_t point_base, int m_begin, int m_end, int flags, void* ws, size_t ws_bytes, void* stream) {
+  WsLayout w;
+  PathArgs a;
+  int rc = label_args(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags & DPI_BOTH, false, nullptr,
+                      ws, ws_bytes, &w, &a);
+  if (rc || n == 0) return rc;
+  if (net->d.kind != 2 || p->td_dt > 0.f) return 0;  // nothing to stage: the fused path kernels do it all
+  return pis_paths(p, net, tx, n, K, a, w, (char*)ws, (hipStream_t)stream, false, true);
 }
 
 int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,

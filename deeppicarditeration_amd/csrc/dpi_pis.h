@@ -3,13 +3,15 @@
 // The 4 x 512 network neither fits in LDS nor keeps per-path activations in registers, so the
 // label path becomes a pipeline over a chunk of R paths (R = rows of every buffer below):
 //   k_pis_rollout   Philox + K-step EM for both paths (as k_paths phase 1), g(X_T) -> a_p;
-//                   writes IN[r] = [.. 64 t_emb slots .., X_s], S_T[r], S_s[r], E[r] = emb(T - s),
-//                   per-path scalars;
-//   k_gemm_nt x 15  t_encoder, smooth_net, nn_module forward, and the vector-Jacobian product of
-//                   nn_module with cotangent X_s (dpi_gemm.h), activations in HBM (fp32);
+//                   writes IN[r] = [.. 64 t_emb slots .., X_s], S_T[r], S_s[r], per-path scalars
+//                   (fp32 rows: also E[r] = emb(T - s));
+//   k_pis_time      (split rows) t_encoder -> IN[:, 0:64] and smooth, weights in LDS, activations
+//                   in registers (fp32 rows: 7 k_gemm_nt launches through E / T1 / H0 / H1);
+//   k_gemm_x3 x 10  nn_module forward and the vector-Jacobian product of nn_module with cotangent
+//                   X_s (dpi_gemm.h), activations in HBM;
 //   k_pis_final     smooth, grad_x u = smooth (J^T X + net_out) + (1 - smooth) e^{-l/2} grad g0,
 //                   f = ffv, b_p, per-path label contributions -> partial slab (fixed-order sums).
-// The per-point baseline runs the same GEMM chain on the n points (k_pis_points, k_pis_base_final).
+// The n per-point baseline rows ride in the first chunk's chain (k_pis_points, k_pis_base_final).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,8 +43,10 @@ struct NetPisDev {
   const uint32_t *te0S, *te2S, *sn0S, *snS[4];
   const uint32_t *nnS[5], *nnTS[5];
   const float* nnbP[5];
+  // [nnT[0] | nn[L]] ((nx -> 64) x (h_0 + h_{L-1})): J^T X + net_out = [D_0 | A_{L-1}] . this^T + b_L
+  const uint32_t* gxnoS;
   // k_gemm_x3 weight scales 2^-s (each split matrix is stored prescaled by 2^s)
-  float te0W, te2W, sn0W, snW[4], nnW[5], nnTW[5];
+  float te0W, te2W, sn0W, snW[4], nnW[5], nnTW[5], gxnoW;
 };
 
 __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float* out /* stride 1 */, int j) {
@@ -52,18 +56,6 @@ __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float*
   sincosf(a, &sn, &cs);
   out[j] = sn;
   out[PIS_CH + j] = cs;
-}
-
-// granule pair (u, q) of the split embedding region: columns c = 32u + 4q + (j & 3) + 16 (j >> 2),
-// sin for c < 64, cos of channel c - 64 above
-__device__ __forceinline__ void pis_embed8(const NetPisDev& pn, float lbd, int u, int q, float (&v)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2), ch = c & (PIS_CH - 1);
-    float sn, cs;
-    sincosf(fmaf(pn.coeff[ch], lbd, pn.phase[ch]), &sn, &cs);
-    v[j] = c < PIS_CH ? sn : cs;
-  }
 }
 
 // Workspace rows of the pipeline (floats per row); every offset a multiple of 4 (fp32 storage) or
@@ -85,16 +77,33 @@ __device__ __forceinline__ float pis_horizon(const EqDev& e, float t, float td_d
   return td_u ? td_dt : e.T - t;
 }
 
+// Dims 4j..4j+3 of a split region starting at word `reg` of a row (a 32-column chunk u = j / 8 holds
+// granule pair q = j % 4 of half h = (j % 8) / 4): 2 hi words and 2 lo words at once.
+__device__ __forceinline__ void x3_put4(float* row, int reg, int j, const float (&v)[4]) {
+  const int u = j >> 3, q = j & 3, h = (j >> 2) & 1;
+  uint32_t hw[2], lw[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const _Float16 h0 = (_Float16)v[2 * p], h1 = (_Float16)v[2 * p + 1];
+    const _Float16 l0 = (_Float16)(v[2 * p] - (float)h0), l1 = (_Float16)(v[2 * p + 1] - (float)h1);
+    hw[p] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    lw[p] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
+  uint32_t* g = reinterpret_cast<uint32_t*>(row + reg) + 32 * u + 8 * q + 2 * h;
+  *reinterpret_cast<uint2*>(g) = make_uint2(hw[0], hw[1]);
+  *reinterpret_cast<uint2*>(g + 4) = make_uint2(lw[0], lw[1]);
+}
+
 template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                      int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
                                                      uint32_t point_base, const float* __restrict__ gx,
                                                      float* __restrict__ rows, PisRows L, int stage, float td_dt) {
+  // 8.7 KB of LDS (no staging of X_s): a rollout block fits on a CU beside a k_gemm_x3 block
+  // (144 KB), so the next batch's rollout can run under this batch's GEMM chain
   __shared__ float xsh[NXP_MAX];
   __shared__ float gsts[4 * P * NSG];
-  __shared__ float xs3[X3 ? P * (NXP_MAX + 1) : 1];  // split mode: X_s staged [path][dim]
-  __shared__ float ssh[X3 ? P : 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = g0 + blockIdx.x;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
@@ -130,20 +139,18 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
         s3 += z.d;
       }
     const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+    float xv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int d = 4 * j + q;
+      xv[q] = d < nx ? fmaf(cT, sv[q], xsh[d]) : 0.f;
       if (d < nx) {
         row[L.ST + d] = sv[q];
-        if (TERM) Eq<KIND>::gstat(e, d, fmaf(cT, sv[q], xsh[d]), gst);
-        if (stage == PIS_TD_TERM) {  // network input X_{t_next}
-          if (X3)
-            xs3[lane * (NXP_MAX + 1) + d] = fmaf(cT, sv[q], xsh[d]);
-          else
-            row[L.IN + PIS_IN_OFF + d] = fmaf(cT, sv[q], xsh[d]);
-        }
+        if (TERM) Eq<KIND>::gstat(e, d, xv[q], gst);
+        if (!X3 && stage == PIS_TD_TERM) row[L.IN + PIS_IN_OFF + d] = xv[q];  // network input X_{t_next}
       }
     }
+    if (X3 && stage == PIS_TD_TERM) x3_put4(row, L.IN + 64, j, xv);
   }
   for (int j = 3 - wv; do_int && j < nb; j += 4) {  // integral path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -156,25 +163,31 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
         s3 += z.d;
       }
     const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+    float xv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int d = 4 * j + q;
+      xv[q] = d < nx ? fmaf(cI, sv[q], xsh[d]) : 0.f;  // X_s
       if (d < nx) {
         row[L.SS + d] = sv[q];
-        if (X3)
-          xs3[lane * (NXP_MAX + 1) + d] = fmaf(cI, sv[q], xsh[d]);
-        else
-          row[L.IN + PIS_IN_OFF + d] = fmaf(cI, sv[q], xsh[d]);  // X_s
+        if (!X3) row[L.IN + PIS_IN_OFF + d] = xv[q];
       }
     }
+    if (X3) x3_put4(row, L.IN + 64, j, xv);
   }
+  // split rows: the zero padding of the x part (dims nx .. INP - 64) of IN
+  if (X3)
+    for (int j = nb + wv; j < (L.INP - 64) / 4; j += 4) {
+      const float z[4] = {0.f, 0.f, 0.f, 0.f};
+      x3_put4(row, L.IN + 64, j, z);
+    }
   // time embedding of lambda = T - s (each wave writes 16 of the 64 channels); the TD terminal
   // stage evaluates the network at t_next
   const float tin = stage == PIS_TD_TERM ? t + td_dt : s;
   if (!X3)
     for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - tin, row + L.E, j);
   else if (wv == 0)
-    ssh[lane] = tin;
+    row[L.SC + 4] = tin;  // k_pis_time evaluates the time networks at T - tin
 #pragma unroll
   for (int c = 0; c < NSG; ++c) gsts[(wv * P + lane) * NSG + c] = gst[c];
   __syncthreads();
@@ -193,26 +206,6 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
       row[L.SC + 3] = smt;
     }
     if (do_term) row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
-  }
-  if constexpr (X3) {  // split rows, whole 32-B granule pairs: X_s -> IN chunks 2.., emb -> E
-    const int nxc = L.INP / 32 - 2;
-    float* rb = rows + (size_t)blockIdx.x * P * L.stride;
-    for (int idx = tid; idx < P * nxc * 4; idx += NTH) {
-      const int p = idx / (nxc * 4), uq = idx - p * (nxc * 4), u = uq >> 2, q = uq & 3;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int d = 32 * u + 4 * q + (j & 3) + 16 * (j >> 2);
-        v[j] = d < nx ? xs3[p * (NXP_MAX + 1) + d] : 0.f;
-      }
-      x3_put8(rb + (size_t)p * L.stride, L.IN, 2 + u, q, v);
-    }
-    for (int idx = tid; idx < P * 16; idx += NTH) {
-      const int p = idx >> 4, u = (idx >> 2) & 3, q = idx & 3;
-      float v[8];
-      pis_embed8(pn, pn.T - ssh[p], u, q, v);
-      x3_put8(rb + (size_t)p * L.stride, L.E, u, q, v);
-    }
   }
 }
 
@@ -236,11 +229,7 @@ __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx,
       }
       x3_put8(row, L.IN, 2 + u, q, v);
     }
-    for (int idx = tid; idx < 16; idx += blockDim.x) {
-      float v[8];
-      pis_embed8(pn, pn.T - txr[0], idx >> 2, idx & 3, v);
-      x3_put8(row, L.E, idx >> 2, idx & 3, v);
-    }
+    if (tid == 0) row[L.SC + 4] = txr[0];
   } else {
     for (int d = tid; d < nx; d += blockDim.x) row[L.IN + PIS_IN_OFF + d] = txr[1 + d];
     for (int j = tid; j < PIS_CH; j += blockDim.x) pis_embed(pn, pn.T - txr[0], row + L.E, j);
@@ -250,6 +239,154 @@ __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx,
     row[L.SC + 1] = 1.f;
     row[L.SC + 2] = 0.f;
     row[L.SC + 3] = 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The time networks of PISGradNet in one launch (split storage): per row lambda = T - tin (tin in
+// SC + 4), emb(lambda) -> t_encoder -> IN[:, 0:64] (split), smooth_net -> smooth (SC + 5), with
+// smooth = smooth_net(emb(lambda))[0] - smooth_net(emb(0))[0] (solution.py:236-254, 268-274).
+// Both networks are 64 channels wide and take one scalar per row, so all their weights (te0, te2,
+// sn0, sn[0..nsm), 144 KB split for nsm = 4) sit in LDS for the whole launch and every layer's
+// activations stay in registers: hidden x path orientation (the units are the MFMA rows, a wave
+// owns 16 paths, the C layout of unit tiles 2u, 2u+1 is the next layer's B operand chunk u, as in
+// mlp_tile_split), three f16 products per fp32 product into one accumulator (the x3 convention of
+// k_gemm_x3: lo unscaled, weights prescaled by 2^s).  Replaces the 7 GEMM launches of the time
+// networks (and their E / T1 / H0 / H1 round trips through HBM).
+// LDS image of a split matrix with Kp words per row (Kp % 64 == 0): logical granule G of row r at
+// (G & ~15) | ((G ^ r) & 15) — every row starts at bank 0, and XOR with the row's low 4 bits gives
+// the 16 lanes of each ds_read_b128 lane group 16 distinct 16-B slots.
+constexpr int PT_THREADS = 512;
+__device__ __forceinline__ int pt_word(int r, int Kp, int G) { return r * Kp + 4 * ((G & ~15) | ((G ^ r) & 15)); }
+
+template <int NSM_MAX>  // LDS holds smooth_net blocks 0..NSM_MAX-1
+__global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float* __restrict__ rows, PisRows L, int R) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  constexpr int C = PIS_CH, W2 = C * 2 * C, W1 = C * C;  // words of a 64 x 128 / 64 x 64 split matrix
+  __shared__ uint32_t wl[2 * W2 + (1 + NSM_MAX) * W1];   // te0 | sn0 | te2 | sn[0..nsm)
+  __shared__ float cph[2 * C];                           // coeff | phase
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, jj = lane & 15, qq = lane >> 4;
+  const int nsm = min(pn.nsm, NSM_MAX);
+  auto stage = [&](const uint32_t* src, int off, int Kp) {
+    const int ng = C * Kp / 4;
+    for (int idx = tid; idx < ng; idx += PT_THREADS) {
+      const int r = idx / (Kp / 4), G = idx - r * (Kp / 4);
+      *reinterpret_cast<u32x4_t*>(wl + off + pt_word(r, Kp, G)) =
+          *reinterpret_cast<const u32x4_t*>(src + (size_t)r * Kp + 4 * G);
+    }
+  };
+  stage(pn.te0S, 0, 2 * C);
+  stage(pn.sn0S, W2, 2 * C);
+  stage(pn.te2S, 2 * W2, C);
+  for (int j = 0; j < nsm; ++j) stage(pn.snS[j], 2 * W2 + (1 + j) * W1, C);
+  if (tid < C) {
+    cph[tid] = pn.coeff[tid];
+    cph[C + tid] = pn.phase[tid];
+  }
+  __syncthreads();
+
+  // acc[T] += W (64 x 32 NU) . B for this wave's 16 paths; B chunk u = (bh[u], bl[u])
+  auto layer = [&](int off, auto NUc, const h8* bh, const h8* bl, f4v (&acc)[4]) {
+    constexpr int NU = decltype(NUc)::value, Kp = 32 * NU;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) acc[T] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int T = 0; T < 4; ++T) {
+        const int r = 16 * T + jj;
+        const h8 ah = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(wl + off + pt_word(r, Kp, 8 * u + 2 * qq)));
+        const h8 al = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(wl + off + pt_word(r, Kp, 8 * u + 2 * qq + 1)));
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[u], acc[T], 0, 0, 0);
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[u], acc[T], 0, 0, 0);
+        acc[T] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[u], acc[T], 0, 0, 0);
+      }
+  };
+  // x3 split of 8 values (lo unscaled)
+  auto split = [&](const float (&v)[8], h8& hi, h8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const _Float16 h = (_Float16)v[j];
+      hi[j] = h;
+      lo[j] = (_Float16)(v[j] - (float)h);
+    }
+  };
+  // activations (C layout, unit 16 T + 4 qq + r) -> B chunks u = 0, 1 (units 32 u + 4 qq + (j & 3) + 16 (j >> 2))
+  auto to_b = [&](const float (&a)[4][4], h8 (&bh)[2], h8 (&bl)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3];
+      split(v, bh[u], bl[u]);
+    }
+  };
+  auto epi = [&](const f4v (&acc)[4], float ws, const float* bias, bool act, float (&a)[4][4]) {
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = fmaf(acc[T][r], ws, bias[16 * T + 4 * qq + r]);
+        a[T][r] = act ? (z > 0.f ? z : __expf(z) - 1.0f) : z;
+      }
+  };
+
+  const int ntiles = (R + 15) >> 4, nwaves = gridDim.x * (PT_THREADS / 64);
+  for (int tile = blockIdx.x * (PT_THREADS / 64) + wv; tile < ntiles; tile += nwaves) {
+    // the LDS weights are loop-invariant: keep the compiler from hoisting every fragment read of
+    // the tile loop into registers (it would need ~600 VGPRs)
+    asm volatile("" ::: "memory");
+    const int pr = min(16 * tile + jj, R - 1);
+    float* row = rows + (size_t)pr * L.stride;
+    const float lbd = pn.T - row[L.SC + 4];
+    // emb(lambda) as the B operand: chunks 0, 1 = sin, 2, 3 = cos of channels 32 u + 4 qq + (j & 3) + 16 (j >> 2)
+    h8 eh[4], el[4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float sv[8], cv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ch = 32 * u + 4 * qq + (j & 3) + 16 * (j >> 2);
+        sincosf(fmaf(cph[ch], lbd, cph[C + ch]), &sv[j], &cv[j]);
+      }
+      split(sv, eh[u], el[u]);
+      split(cv, eh[2 + u], el[2 + u]);
+    }
+    f4v acc[4];
+    float a[4][4];
+    h8 bh[2], bl[2];
+    // t_encoder: Linear(128, 64), ELU, Linear(64, 64) -> IN[:, 0:64]
+    layer(0, std::integral_constant<int, 4>{}, eh, el, acc);
+    epi(acc, pn.te0W, pn.te0b, true, a);
+    to_b(a, bh, bl);
+    layer(2 * W2, std::integral_constant<int, 2>{}, bh, bl, acc);
+    epi(acc, pn.te2W, pn.te2b, false, a);
+    if (16 * tile + jj < R) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3];
+        x3_put8(row, L.IN, u, qq, v);
+      }
+    }
+    // smooth_net: Linear(128, 64), nsm x (ELU, Linear(64, 64)), ELU, row 0 of Linear(64, dim)
+    layer(W2, std::integral_constant<int, 4>{}, eh, el, acc);
+    epi(acc, pn.sn0W, pn.sn0b, true, a);
+    for (int j = 0; j < nsm; ++j) {
+      to_b(a, bh, bl);
+      layer(2 * W2 + (1 + j) * W1, std::integral_constant<int, 2>{}, bh, bl, acc);
+      epi(acc, pn.snW[j], pn.snb[j], true, a);
+    }
+    float sr = 0.f;
+#pragma unroll
+    for (int T = 0; T < 4; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sr = fmaf(pn.snlast[16 * T + 4 * qq + r], a[T][r], sr);
+    sr += __shfl_xor(sr, 16, 64);
+    sr += __shfl_xor(sr, 32, 64);
+    if (qq == 0 && 16 * tile + jj < R) row[L.SC + 5] = sr + pn.snlastb[0] - pn.smooth0;
   }
 }
 
@@ -285,30 +422,20 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
   int nxc = 0;
   if constexpr (X3) {
     nxc = L.INP / 32 - 2;
-    float hv[PIS_CH / 32][8];
-#pragma unroll
-    for (int u = 0; u < PIS_CH / 32; ++u) x3_get8(row, L.H0, u, q, hv[u]);
 #pragma unroll
     for (int u = 0; u < NXC; ++u) {
       if (u < nxc) {
-        float gv[8], nv[8];
         x3_get8(row, L.IN, 2 + u, q, xs[u]);
-        x3_get8(row, L.GX, u, q, gv);
-        x3_get8(row, L.NO, u, q, nv);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) js[u][j] = gv[j] + nv[j];
+        x3_get8(row, L.GX, u, q, js[u]);  // split chain: GX = J^T X + net_out in one GEMM
       }
     }
-#pragma unroll
-    for (int u = 0; u < PIS_CH / 32; ++u)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], hv[u][j], sr);
   } else {
     for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
   }
   sr += __shfl_xor(sr, 1, 64);
   sr += __shfl_xor(sr, 2, 64);
-  const float smooth = sr + pn.snlastb[0] - pn.smooth0;
+  // split rows: smooth from k_pis_time
+  const float smooth = X3 ? row[L.SC + 5] : sr + pn.snlastb[0] - pn.smooth0;
   const float decay = __expf(-0.5f * lbd);
   // visit(d, X_d, (J^T X + net_out)_d) over this thread's dims
   auto for_dims = [&](auto&& visit) {
@@ -412,20 +539,11 @@ __global__ void k_pis_tvalue(EqDev e, NetPisDev pn, const float* __restrict__ tx
   const float lbd = pn.T - (t + td_dt);
   // smooth (as pis_z_stats)
   float sr = 0.f;
-  if constexpr (X3) {
-#pragma unroll
-    for (int u = 0; u < PIS_CH / 32; ++u) {
-      float v[8];
-      x3_get8(row, L.H0, u, q, v);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sr = fmaf(pn.snlast[32 * u + 4 * q + (j & 3) + 16 * (j >> 2)], v[j], sr);
-    }
-  } else {
+  if constexpr (!X3)
     for (int k = q; k < PIS_CH; k += 4) sr = fmaf(pn.snlast[k], row[L.H0 + k], sr);
-  }
   sr += __shfl_xor(sr, 1, 64);
   sr += __shfl_xor(sr, 2, 64);
-  const float smooth = sr + pn.snlastb[0] - pn.smooth0;
+  const float smooth = X3 ? row[L.SC + 5] : sr + pn.snlastb[0] - pn.smooth0;  // split: from k_pis_time
   const float decay = __expf(-0.5f * lbd);
   float sp = 0.f, st[NSG];
 #pragma unroll

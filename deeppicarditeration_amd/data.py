@@ -281,6 +281,16 @@ class OnlineDataGenerator:
                                               ws.numel(), _stream(self._device)), "dpi_label_moments")
         return mom
 
+    def label_prepare(self, tx, point_base, M, m_begin, m_end, flags, ws):
+        """First half of label_moments that needs no network evaluation of this batch (PISGradNet:
+        the first path chunk's rollout; a no-op otherwise), so it can run on a side stream under the
+        previous batch's network work.  The matching label_moments call passes flags | DPI_PREPARED."""
+        n = tx.shape[0]
+        self._configure_problem()
+        _lib.check(self.lib.dpi_label_prepare(self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed,
+                                              self.epoch, point_base, m_begin, m_end, flags, _ptr(ws), ws.numel(),
+                                              _stream(self._device)), "dpi_label_prepare")
+
     def finalize(self, moments, M, flags, ws, bound=None):
         n = moments.shape[0]
         y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self._device)

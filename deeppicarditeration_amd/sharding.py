@@ -62,11 +62,15 @@ class ShardedLabeler:
         return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
 
     # ------------------------------------------------------------------ two-phase (pipelined) labels
-    def prepare(self, n):
-        """Sample the next batch's points and their per-point baseline on a side stream, into one of
-        three workspaces, so both run while the current stream still executes the previous batch's
-        moments (the baseline is a handful of latency-bound blocks that otherwise serialise between
-        two path launches).  Returns the handle for begin(prepared=...)."""
+    def prepare(self, n, flags=None):
+        """Sample the next batch's points, their per-point baseline and (PISGradNet) the first path
+        chunk's rollout on a side stream, into one of three workspaces, so they run while the
+        current stream still executes the previous batch's moments: the baseline is a handful of
+        latency-bound blocks that otherwise serialise between two path launches, and the VALU-bound
+        rollout fits on each CU beside a k_gemm_x3 block of the previous batch's MFMA-bound GEMM
+        chain.  Returns the handle for begin(prepared=...)."""
+        from . import _lib
+        flags = _lib.DPI_BOTH if flags is None else flags
         gen = self.gen
         cur = torch.cuda.current_stream(gen.device)
         M = gen.n_estimate_integral
@@ -87,10 +91,12 @@ class ShardedLabeler:
                 self._side.wait_event(self._prep_free[k])
             tx, pb = gen.sample_t_and_x(n)
             gen.point_baseline(tx, ws=ws)
+            m0, m1 = self.shard(M)
+            gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
             ready = torch.cuda.Event()
             ready.record(self._side)
         tx.record_stream(cur)
-        return tx, pb, ws, ready, k
+        return tx, pb, ws, ready, k, flags
 
     def begin(self, tx=None, point_base=None, flags=None, on_moments_begin=None, on_moments_end=None,
               prepared=None):
@@ -99,13 +105,17 @@ class ShardedLabeler:
         kernels while it is in flight).  Two workspaces alternate (three with prepare()), so one
         batch may be pending while the next begins.  Returns the handle end() turns into labels."""
         from . import _lib
-        flags = _lib.DPI_BOTH if flags is None else flags
         M = self.gen.n_estimate_integral
         if self.gen.n_estimate_terminal != M:
             raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
         slot = wslot = None
+        kflags = None
         if prepared is not None:
-            tx, point_base, ws, ready, slot = prepared
+            tx, point_base, ws, ready, slot, pflags = prepared
+            if flags is not None and flags != pflags:
+                raise ValueError(f"begin(flags={flags}) on a batch prepared with flags={pflags}")
+            flags = pflags
+            kflags = flags | _lib.DPI_PREPARED
             torch.cuda.current_stream(self.gen.device).wait_event(ready)
         else:
             n = tx.shape[0]
@@ -123,10 +133,11 @@ class ShardedLabeler:
             ws = self._ws_pool[wslot]
             self._ws_next ^= 1
             self.gen.point_baseline(tx, ws=ws)
+        flags = _lib.DPI_BOTH if flags is None else flags
         m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
-        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags, ws)
+        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags if kflags is None else kflags, ws)
         if on_moments_end:
             on_moments_end()
         if self.world == 1:

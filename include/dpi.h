@@ -72,6 +72,8 @@ extern "C" {
 #define DPI_TERMINAL 1 /* estimate_terminal_with_gradients (data.py:899-926) */
 #define DPI_INTEGRAL 2 /* estimate_integral_with_gradients (data.py:471-527) */
 #define DPI_BOTH 3     /* generate_with_gradients (data.py:1208-1218) */
+/* dpi_label_moments: dpi_label_prepare already ran on this workspace with the same arguments */
+#define DPI_PREPARED 4
 
 /* Monte-Carlo paths per workgroup: m ranges are multiples of this. */
 #define DPI_PATH_BLOCK 64
@@ -161,6 +163,17 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
 int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                       uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                       void* ws, size_t ws_bytes, void* stream);
+
+/* Optional first half of dpi_label_moments, for pipelining consecutive batches: the stages that
+ * need no network evaluation of this batch's paths and can therefore run on a side stream while the
+ * previous batch's network work still occupies the GPU.  For a PISGradNet net (non-TD estimators)
+ * that is the first path chunk's Philox + K-step Euler-Maruyama rollout and the baseline rows
+ * (data.py:471-527, 899-926 up to the network call); for the fused-kernel nets it is a no-op.  Same
+ * arguments as dpi_label_moments (after dpi_point_baseline on the same workspace); the matching
+ * dpi_label_moments call then passes flags | DPI_PREPARED. */
+int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                      uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, void* ws,
+                      size_t ws_bytes, void* stream);
 
 /* parts: (n_parts, n, 2, 1+nx) -> out (n, 2, 1+nx) with the same pairwise tree as
  * dpi_label_moments' block sum.  `parts` is read only. */

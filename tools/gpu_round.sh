@@ -25,6 +25,13 @@ for w in $what; do
     done
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
       python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline --no-prepare > $out/trace_hjb_onestream.log 2>&1 ;;
+  hjb)
+    run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
+      python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline --no-prepare > $out/trace_hjb_onestream.log 2>&1 ;;
+  hjbprep)
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_prepare -o trace --output-format csv -- \
+      python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_hjb_prepare.log 2>&1 ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
   pmc)

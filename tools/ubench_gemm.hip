@@ -953,10 +953,10 @@ int main(int argc, char** argv) {
     for (int i = 0; i < iters; ++i) {
       if (epi == 1)
         hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
-                           1.0f / 16.0f, XU, Kp, dst, Np, bias, AUXU, Np);
+                           1.0f / 16.0f, XU, Kp, XU, Kp, Kp / 32, dst, Np, bias, AUXU, Np);
       else
         hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, M, Kp, nnt, WU,
-                           1.0f / 16.0f, XU, Kp, dst, Np, nullptr, AUXU, Np);
+                           1.0f / 16.0f, XU, Kp, XU, Kp, Kp / 32, dst, Np, nullptr, AUXU, Np);
     }
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
