@@ -222,28 +222,36 @@ constexpr int X3_BM = 256, X3_STAGES = 3, X3_THREADS = 512;
 // VAR (schedule experiments, tools/ubench_x3.hip; 0 = product): bit 0 s_setprio 1 for waves 4-7,
 // bit 1 fragment reads front-loaded into the first 2/3 of the MFMAs, bit 2 the DMA issue interleaved
 // with the first MFMAs.
-template <int EPI, int NT, int VAR = 0>
-__global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
-                                                           float wscale, const float* __restrict__ X, int ldx,
-                                                           const float* __restrict__ X2, int ldx2, int nk1,
-                                                           float* __restrict__ OUT, int ldc,
-                                                           const float* __restrict__ bias,
-                                                           const float* __restrict__ AUX, int ldaux) {
+// XCD-aware bijective remap (dispatch puts block b on XCD b % 8): the n-tiles of one m-tile run
+// back to back on one XCD
+__device__ __forceinline__ int x3_tile_of_block() {
+  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+}
+
+template <int NT>
+struct X3Lds {
+  static constexpr int BN = 32 * NT, STAGE = (BN + X3_BM) * 32;
+  uint32_t sm[X3_STAGES * STAGE];
+};
+
+// One 256 x BN output tile (rows m0.., units n0..) of the split GEMM, the whole K loop and the
+// epilogue; `sm` is the block's LDS ring (free on entry, free again on return).
+template <int EPI, int NT, int VAR>
+__device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n0, int M, int Kp,
+                                        const uint32_t* __restrict__ W, float wscale, const float* __restrict__ X,
+                                        int ldx, const float* __restrict__ X2, int ldx2, int nk1,
+                                        float* __restrict__ OUT, int ldc, const float* __restrict__ bias,
+                                        const float* __restrict__ AUX, int ldaux) {
   static_assert(NT == 2 || NT == 4, "wave n-tiles");
   constexpr int BN = 32 * NT, BM = X3_BM, STAGE = (BN + BM) * 32, NWAVE = X3_THREADS / 64;
   constexpr int NINS = (BN + BM) / 8, PER_WAVE = NINS / NWAVE;  // DMA wave-instructions per chunk
   static_assert(NINS % NWAVE == 0 && (PER_WAVE == 6 || PER_WAVE == 5), "DMA split / vmcnt immediates");
-  __shared__ uint32_t sm[X3_STAGES * STAGE];
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
   typedef float f4v __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
   const int il = lane & 15, ql = lane >> 4;
-  // XCD-aware bijective remap (dispatch puts block b on XCD b % 8)
-  const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
-  const int m0 = mt * BM, n0 = nt * BN;
   const int nk = Kp >> 5;
   const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
   const uint32_t* X2w = reinterpret_cast<const uint32_t*>(X2);
@@ -400,6 +408,20 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
     }
   }
 }
+
+template <int EPI, int NT, int VAR = 0>
+__global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
+                                                           float wscale, const float* __restrict__ X, int ldx,
+                                                           const float* __restrict__ X2, int ldx2, int nk1,
+                                                           float* __restrict__ OUT, int ldc,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ AUX, int ldaux) {
+  __shared__ X3Lds<NT> lds;
+  const int tile = x3_tile_of_block(), mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+  x3_tile<EPI, NT, VAR>(lds.sm, mt * X3_BM, nt * 32 * NT, M, Kp, W, wscale, X, ldx, X2, ldx2, nk1, OUT, ldc, bias, AUX,
+                        ldaux);
+}
+
 
 
 }  // namespace dpi

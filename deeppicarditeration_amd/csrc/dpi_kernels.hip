@@ -834,18 +834,21 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   int Kp = L.INP;
   const float* a = rows + L.IN;
   for (int l = 0; l < pd.L; ++l) {
-    gemm_x3(EPI_BIAS_ELU, R, Kp, r64(pd.h[l]), pd.nnS[l], pd.nnW[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, st);
+    const int Np = r64(pd.h[l]);
+    gemm_x3(EPI_BIAS_ELU, R, Kp, Np, pd.nnS[l], pd.nnW[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, st);
     a = rows + L.A[l];
-    Kp = r64(pd.h[l]);
+    Kp = Np;
   }
   if (!vjp) {  // forward only (TD terminal value): net_out
     gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
     return L;
   }
-  // VJP: the x part of IN starts at its chunk 2 (word 64)
+  // VJP: the x part of IN starts at its chunk 2 (word 64).  (Fusing this product into the last
+  // forward layer's launch, elu' read back from the tile the block had just stored, measured no
+  // faster: 828 us against 487 + 335 us.)
   int dcur = L.D0, dnext = L.D1;
-  gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], pd.nnTW[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld, nullptr,
-          rows + L.A[pd.L - 1], ld, st);
+  gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], pd.nnTW[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld,
+          nullptr, rows + L.A[pd.L - 1], ld, st);
   for (int l = pd.L - 1; l >= 1; --l) {
     gemm_x3(EPI_DELU, R, r64(pd.h[l]), r64(pd.h[l - 1]), pd.nnTS[l], pd.nnTW[l], rows + dcur, ld, rows + dnext, ld, nullptr,
             rows + L.A[l - 1], ld, st);
@@ -1026,7 +1029,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     if (prepare_only) return;
     const PisRows Lc = chain(true, g * P + (base ? n : 0));
     if (base)
-      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 15) / 16), dim3(64), 0, st, p->e, net->pis,
+      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 63) / 64), dim3(256), 0, st, p->e, net->pis,
                          brows, Lc, n, fb);
     hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
                        a.flags, fb, rows, Lc, a.partial, dt);

@@ -256,7 +256,7 @@ __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx,
 // LDS image of a split matrix with Kp words per row (Kp % 64 == 0): logical granule G of row r at
 // (G & ~15) | ((G ^ r) & 15) — every row starts at bank 0, and XOR with the row's low 4 bits gives
 // the 16 lanes of each ds_read_b128 lane group 16 distinct 16-B slots.
-constexpr int PT_THREADS = 512;
+constexpr int PT_THREADS = 768;  // 12 waves: 3 per SIMD at <= 168 VGPRs
 __device__ __forceinline__ int pt_word(int r, int Kp, int G) { return r * Kp + 4 * ((G & ~15) | ((G ^ r) & 15)); }
 
 template <int NSM_MAX>  // LDS holds smooth_net blocks 0..NSM_MAX-1
@@ -505,14 +505,15 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
   smooth_out = smooth;
 }
 
-// Baseline f_b (state part) and nothing else: one 64-thread block per 16 points.
+// Baseline f_b (state part) and nothing else: one 256-thread block per 64 points (4 threads per
+// point; a latency chain, so the GMM staging is spread over all 256 threads).
 template <int KIND, bool X3>
-__global__ __launch_bounds__(64) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L, int n,
-                                 float* __restrict__ fb) {
+__global__ __launch_bounds__(256) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L,
+                                                        int n, float* __restrict__ fb) {
   __shared__ PisGmmLds gmm;
   pis_stage_gmm(e, gmm);
   __syncthreads();
-  const int i = blockIdx.x * 16 + (threadIdx.x >> 2), q = threadIdx.x & 3;
+  const int i = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
   const int ic = min(i, n - 1);
   const float* row = rows + (size_t)ic * L.stride;
   float A, B, sm;
@@ -597,7 +598,8 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
                                                    int nbp, int K, int flags, const float* __restrict__ fbv,
                                                    const float* __restrict__ rows, PisRows L,
                                                    float* __restrict__ partial, float td_dt) {
-  __shared__ float cs[2][P][NXP_MAX + 4];  // per-path contributions and their squares: [path][col]
+  __shared__ float part[4][4][64];  // per-wave 16-path column sums: [wave][q][value]
+  __shared__ float vsum[4][2];      // per-wave sums of the value column and its square
   __shared__ PisGmmLds gmm;
   pis_stage_gmm(e, gmm);
   __syncthreads();
@@ -617,30 +619,54 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
   const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * smt) * e.asq);
-  if (q == 0) {
-    const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
-    cs[0][p][0] = c0;
-    cs[1][p][0] = c0 * c0;
-  }
+  // this row's contributions: v[2k + mom] for dim d = q + 4k (k < 32: nx <= 128), the value column
+  // (lane group q = 0) apart
+  static_assert(NXP_MAX <= 128, "dims per lane group");
+  float v[64];
   const float aY = ap * yT, bY = bp * yI;
-  for (int d = q; d < nx; d += 4) {
-    const float v = fmaf(aY, row[L.ST + d], bY * row[L.SS + d]);
-    cs[0][p][1 + d] = v;
-    cs[1][p][1 + d] = v * v;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const int d = q + 4 * k;
+    const float c = d < nx ? fmaf(aY, row[L.ST + d], bY * row[L.SS + d]) : 0.f;
+    v[2 * k] = c;
+    v[2 * k + 1] = c * c;
+  }
+  float c0 = q == 0 ? ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f) : 0.f, c0s = c0 * c0;
+  // sum over the wave's 16 rows (lane = 4 row + q) by a halving butterfly on lane bits 5..2: at bit
+  // m a lane keeps the half of its values selected by that bit and adds its partner's copy, so lane
+  // (row r, q) ends with values 4r .. 4r + 3 summed over the 16 rows of lane group q
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int bit = 5; bit >= 2; --bit) {  // the value column: a plain xor tree over the same lane bits
+    c0 += __shfl_xor(c0, 1 << bit, 64);
+    c0s += __shfl_xor(c0s, 1 << bit, 64);
+  }
+#define DPI_HALVE(BIT, H)                                          \
+  _Pragma("unroll") for (int j = 0; j < H; ++j) {                  \
+    const bool up = (lane >> BIT) & 1;                             \
+    const float keep = up ? v[j + H] : v[j];                       \
+    const float send = up ? v[j] : v[j + H];                       \
+    v[j] = keep + __shfl_xor(send, 1 << BIT, 64);                  \
+  }
+  DPI_HALVE(5, 32)
+  DPI_HALVE(4, 16)
+  DPI_HALVE(3, 8)
+  DPI_HALVE(2, 4)
+#undef DPI_HALVE
+#pragma unroll
+  for (int j = 0; j < 4; ++j) part[wv][q][4 * (lane >> 2) + j] = v[j];
+  if (lane == 0) {
+    vsum[wv][0] = c0;
+    vsum[wv][1] = c0s;
   }
   __syncthreads();
-  // fixed-order (pairwise) sum over the 64 paths of each column
+  // the four waves' sums, (w0 + w1) + (w2 + w3): a fixed order independent of rank and chunk
   float* out = partial + ((size_t)i * nbp + b) * slab_row(F);  // [point][block][slab_row(F)]
-  for (int c = tid; c < 2 * F; c += NTH) {
-    const int mom = c >= F, col = c - mom * F;
-    float v[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = cs[mom][k][col];
-#pragma unroll
-    for (int w = 1; w < P; w <<= 1)
-#pragma unroll
-      for (int k = 0; k < P; k += 2 * w) v[k] += v[k + w];
-    out[c] = v[0];
+  {
+    const int qq = tid >> 6, j = tid & 63, k = j >> 1, mom = j & 1;
+    const float sum = (part[0][qq][j] + part[1][qq][j]) + (part[2][qq][j] + part[3][qq][j]);
+    if (qq + 4 * k < nx) out[mom * F + 1 + qq + 4 * k] = sum;
+    if (tid < 2) out[tid * F] = (vsum[0][tid] + vsum[1][tid]) + (vsum[2][tid] + vsum[3][tid]);
   }
 }
 
