@@ -348,6 +348,9 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
   };
   if constexpr (VAR & 1)
     if (wv >= 4) __builtin_amdgcn_s_setprio(1);
+  // above any co-resident wave of another kernel (the prepare stream's rollout): the
+  // GEMM's issue comes first, the VALU-bound rollout takes the cycles the GEMM leaves
+  if constexpr (!(VAR & 1)) __builtin_amdgcn_s_setprio(2);
   // prologue: chunks 0, 1, 2 (clamped) in flight; publish chunk 0 and read it
   issue(0, 0);
   issue(min(1, nk - 1), 1);

@@ -1007,9 +1007,18 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       return X3 ? pis_chain_x3(net->pis, rows, R, st, vjp) : pis_chain(net->pis, rows, R, st, vjp);
     };
     auto rollout = [&](int stage) {
-      hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp,
-                         a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L, stage,
-                         dt);
+      // prepare stream: grids of one block per CU, so the rollout takes one wave per SIMD beside the
+      // previous batch's GEMM blocks instead of packing whole CUs (which starves the GEMM)
+      int step = g;
+      if (prepare_only) {
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        step = std::max(1, ncu);
+      }
+      for (int bx0 = 0; bx0 < g; bx0 += step)
+        hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
+                           net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
+                           a.point_base, a.gx, rows, L, stage, dt, bx0);
     };
     const bool base = g0 == 0;
     float* brows = rows + (size_t)g * P * L.stride;

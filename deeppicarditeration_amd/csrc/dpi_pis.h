@@ -94,18 +94,16 @@ __device__ __forceinline__ void x3_put4(float* row, int reg, int j, const float 
   *reinterpret_cast<uint2*>(g + 4) = make_uint2(lw[0], lw[1]);
 }
 
+// One (point, 64-path block) of the rollout: bx = the block's index within the chunk.
 template <int KIND, bool X3>
-__global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
-                                                     int nbp, int m_begin, int K, int flags, uint32_t k0,
-                                                     uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
-                                                     uint32_t point_base, const float* __restrict__ gx,
-                                                     float* __restrict__ rows, PisRows L, int stage, float td_dt) {
-  // 8.7 KB of LDS (no staging of X_s): a rollout block fits on a CU beside a k_gemm_x3 block
-  // (144 KB), so the next batch's rollout can run under this batch's GEMM chain
-  __shared__ float xsh[NXP_MAX];
-  __shared__ float gsts[4 * P * NSG];
+__device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
+                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
+                                                  uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
+                                                  uint32_t point_base, const float* __restrict__ gx,
+                                                  float* __restrict__ rows, const PisRows& L, int stage, float td_dt,
+                                                  float* xsh, float* gsts, int bx) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int g = g0 + blockIdx.x;  // (point, block) in point-major order
+  const int g = g0 + bx;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
   const uint32_t ig = point_base + (uint32_t)i;
   const uint32_t m = (uint32_t)(m_begin + P * blk + lane);
@@ -117,7 +115,7 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
   bool td_u;
   const float tmt = pis_horizon(e, t, td_dt, td_u);
   for (int d = tid; d < NXP_MAX; d += NTH) xsh[d] = d < nx ? txr[1 + d] : 0.f;
-  const size_t r = (size_t)blockIdx.x * P + lane;
+  const size_t r = (size_t)bx * P + lane;
   float* row = rows + r * L.stride;
   const float U = u01_oc(philox4x32_10(0u, m, ig, c3s, k0, k1).x);
   const float s = fmaf(U, tmt, t);
@@ -207,6 +205,22 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
     }
     if (do_term) row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
   }
+}
+
+// Block bx0 + blockIdx.x of the chunk.  8.7 KB of LDS (no staging of X_s) and 40 VGPRs, so a
+// rollout block (one wave per SIMD) fits on a CU beside a k_gemm_x3 block (144 KB, 2 x 232 VGPRs
+// per SIMD): the prepare stream launches the next batch's rollout in grids of one block per CU.
+template <int KIND, bool X3>
+__global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
+                                                     int nbp, int m_begin, int K, int flags, uint32_t k0,
+                                                     uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
+                                                     uint32_t point_base, const float* __restrict__ gx,
+                                                     float* __restrict__ rows, PisRows L, int stage, float td_dt,
+                                                     int bx0) {
+  __shared__ float xsh[NXP_MAX];
+  __shared__ float gsts[4 * P * NSG];
+  pis_rollout_block<KIND, X3>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L,
+                              stage, td_dt, xsh, gsts, bx0 + blockIdx.x);
 }
 
 // Baseline rows: IN[i] = [.., x], E[i] = emb(T - t), SC = (t, 1, 0, 0).

@@ -267,6 +267,38 @@ __global__ __launch_bounds__(X4_THREADS, 1) void k_gemm_x4(int M, int Kp, int n_
 
 }  // namespace dpi
 
+
+// Persistent walk of the product tile body (x3_tile), G blocks (one per CU), block b takes the
+// virtual blocks v = b + j G through the same XCD remap as the product; STAG > 0: blocks whose
+// in-XCD index is odd (STAG = 2) or = 1, 2, 3 mod 4 (STAG = 4) first sleep that fraction of a tile
+// (TILE_CYC cycles), so that the CUs' epilogue store bursts do not all coincide.
+namespace dpi {
+template <int EPI, int STAG>
+__global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3s(int M, int Kp, int n_ntiles, int n_tiles,
+                                                            const uint32_t* __restrict__ W, float wscale,
+                                                            const float* __restrict__ X, int ldx, float* __restrict__ OUT,
+                                                            int ldc, const float* __restrict__ bias,
+                                                            const float* __restrict__ AUX, int ldaux, int tile_cyc) {
+  __shared__ X3Lds<4> lds;
+  const int G = gridDim.x, b = blockIdx.x;
+  if (STAG > 0) {
+    const int ph = (b >> 3) % STAG;
+    const long long until = (long long)tile_cyc * ph / STAG;
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t0 < until) __builtin_amdgcn_s_sleep(32);
+  }
+  const int q8 = n_tiles >> 3, r8 = n_tiles & 7;
+  for (int v = b; v < n_tiles; v += G) {
+    const int xcd = v & 7, loc = v >> 3;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+    x3_tile<EPI, 4, 0>(lds.sm, mt * X3_BM, nt * 128, M, Kp, W, wscale, X, ldx, X, ldx, Kp >> 5, OUT, ldc,
+                       EPI == EPI_DELU ? nullptr : bias, AUX, ldaux);
+    __syncthreads();
+  }
+}
+}  // namespace dpi
+
 using namespace dpi;
 
 #define CK(x)                                                                   \
@@ -301,10 +333,14 @@ struct Bufs {
   float *X, *AUX, *OUT, *REF, *bias;
 };
 
-// VAR 100: k_gemm_x4 (256 x 256 tile, one wave per SIMD)
+// VAR 100+: k_gemm_x4 (256 x 256 tile, one wave per SIMD); VAR 200 + STAG: persistent x3_tile walk
 template <int EPI, int VAR>
 static void launch(const Bufs& b, float* out) {
-  if constexpr (VAR >= 100) {
+  if constexpr (VAR >= 200) {
+    const int nnt = b.Np / 128, nmt = (b.M + X3_BM - 1) / X3_BM;
+    hipLaunchKernelGGL((k_gemm_x3s<EPI, VAR - 200>), dim3(256), dim3(X3_THREADS), 0, 0, b.M, b.Kp, nnt, nnt * nmt, b.W,
+                       1.0f / 16.0f, b.X, b.Kp, out, b.Np, b.bias, b.AUX, b.Np, 27000 * 2);
+  } else if constexpr (VAR >= 100) {
     const int nnt = b.Np / X4_BN, nmt = (b.M + X4_BM - 1) / X4_BM;
     hipLaunchKernelGGL((k_gemm_x4<EPI, VAR - 100>), dim3(nnt * nmt), dim3(X4_THREADS), 0, 0, b.M, b.Kp, nnt, b.W, 1.0f / 16.0f,
                        b.X, b.Kp, b.X, b.Kp, b.Kp / 32, out, b.Np, EPI == EPI_DELU ? nullptr : b.bias, b.AUX, b.Np);
@@ -447,6 +483,23 @@ int main(int argc, char** argv) {
         e3 = std::max(e3, std::fabs(dec(&o3[(size_t)m * b.Np], n) - ref));
       }
       std::printf("row %2d: max|x4 - cpu| %.3e  max|product - cpu| %.3e\n", m, e4, e3);
+    }
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "stag") == 0) {
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
+      launch<EPI_BIAS_ELU, 0>(b, b.REF);
+      run<EPI_BIAS_ELU, 0>("product", b, iters);
+      run<EPI_BIAS_ELU, 200>("persistent x3_tile walk", b, iters);
+      run<EPI_BIAS_ELU, 202>("persistent, 2-phase stagger", b, iters);
+      run<EPI_BIAS_ELU, 204>("persistent, 4-phase stagger", b, iters);
+      CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
+      launch<EPI_DELU, 0>(b, b.REF);
+      run<EPI_DELU, 0>("product", b, iters);
+      run<EPI_DELU, 200>("persistent x3_tile walk", b, iters);
+      run<EPI_DELU, 202>("persistent, 2-phase stagger", b, iters);
+      run<EPI_DELU, 204>("persistent, 4-phase stagger", b, iters);
     }
     return 0;
   }
