@@ -47,6 +47,8 @@ SIGNATURES = {
     "dpi_point_baseline": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     "dpi_label_moments": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
                                   c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "dpi_label_moments_finalize": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
+                                           c_uint32, c_int, c_float, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "dpi_label_prepare": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
                                   c_int, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "dpi_moments_reduce": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

@@ -93,6 +93,27 @@ __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ h
   }
 }
 
+// The same sums for nbp <= 64 with one THREAD per (point, column): consecutive threads read
+// consecutive columns (coalesced; the wave-per-column form above reads 16 floats 40 KB apart per
+// wave), and the 64-leaf tree runs in registers — for nbp <= 64, tree_sum is exactly the perfect
+// binary tree over 64 zero-padded leaves, so the results are bitwise those of k_reduce_hess.
+__global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__ hpart, int n, int C, int nbp,
+                                                       float* __restrict__ hsum, float invM, float bound,
+                                                       float* __restrict__ y, int ystride, int yoff) {
+  const int i = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* p = hpart + (size_t)i * nbp * C + c;
+  float v[64];
+#pragma unroll
+  for (int b = 0; b < 64; ++b) v[b] = b < nbp ? p[(size_t)b * C] : 0.f;
+#pragma unroll
+  for (int w = 1; w < 64; w <<= 1)
+#pragma unroll
+    for (int b = 0; b < 64; b += 2 * w) v[b] = v[b] + v[b + w];
+  if (hsum) hsum[(size_t)i * C + c] = v[0];
+  if (y) y[(size_t)i * ystride + yoff + c] = clip_label(v[0] * invM, bound);
+}
+
 // Hessian sums (n, C) -> y[:, off:off+C] = clip(sum / M)
 __global__ void k_finalize_hess(const float* __restrict__ hsum, int n, int C, float invM, float bound,
                                 float* __restrict__ y, int ystride, int yoff) {
@@ -1166,6 +1187,14 @@ int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M,
                       stream, nullptr, 0.f);
 }
 
+int dpi_label_moments_finalize(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                               uint32_t epoch, uint32_t point_base, int flags, float sample_bound, float* y,
+                               float* moments, void* ws, size_t ws_bytes, void* stream) {
+  if (n > 0 && !y) return fail(DPI_ERR_ARG, "label_moments_finalize: null y");
+  return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, moments, ws, ws_bytes, stream, y,
+                      sample_bound);
+}
+
 int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, void* stream) {
   if (n < 0 || (n && (!parts || !out)) || n_parts < 1 || nx < 1) return fail(DPI_ERR_ARG, "moments_reduce: bad arguments");
   if (n == 0) return 0;
@@ -1281,7 +1310,11 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
                      1.0f / (float)M, 1, bound, y, F + C);
-  hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
+  if (nbp <= 64)
+    hipLaunchKernelGGL(k_reduce_hess64, dim3((C + 255) / 256, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
+                     1.0f / (float)M, bound, y, F + C, F);
+  else
+    hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
                      1.0f / (float)M, bound, y, F + C, F);
   HIPCHK(hipGetLastError());
   return 0;

@@ -281,6 +281,19 @@ class OnlineDataGenerator:
                                               ws.numel(), _stream(self._device)), "dpi_label_moments")
         return mom
 
+    def label_moments_finalize(self, tx, point_base, M, flags, ws, bound=None):
+        """label_moments over all of [0, M) and finalize in the same reduce launch -> (y, moments)."""
+        n = tx.shape[0]
+        mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
+        y = torch.empty(n, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
+        b = self.sample_bound if bound is None else bound
+        self._configure_problem()
+        _lib.check(self.lib.dpi_label_moments_finalize(self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed,
+                                                       self.epoch, point_base, flags, b, _ptr(y), _ptr(mom), _ptr(ws),
+                                                       ws.numel(), _stream(self._device)),
+                   "dpi_label_moments_finalize")
+        return y, mom
+
     def label_prepare(self, tx, point_base, M, m_begin, m_end, flags, ws):
         """First half of label_moments that needs no network evaluation of this batch (PISGradNet:
         the first path chunk's rollout; a no-op otherwise), so it can run on a side stream under the

@@ -137,11 +137,14 @@ class ShardedLabeler:
         m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
+        if self.world == 1:  # one rank: the labels come out of the moments' reduce launch
+            y, _ = self.gen.label_moments_finalize(tx, point_base, M, flags if kflags is None else kflags, ws)
+            if on_moments_end:
+                on_moments_end()
+            return (None, y, None, None, flags, M, slot, wslot)  # ws None: y final (end() only recycles)
         mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags if kflags is None else kflags, ws)
         if on_moments_end:
             on_moments_end()
-        if self.world == 1:
-            return (ws, mom, None, None, flags, M, slot, wslot)
         import torch.distributed as dist
         mom = mom.contiguous()
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
@@ -151,10 +154,13 @@ class ShardedLabeler:
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
         ws, mom, work, shape, flags, M, slot, wslot = pending
-        if work is not None:
-            work.wait()  # the current stream waits for RCCL's, not the host
-            mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
-        y = self.gen.finalize(mom, M, flags, ws)
+        if ws is None:  # one rank: begin() already finalized
+            y = mom
+        else:
+            if work is not None:
+                work.wait()  # the current stream waits for RCCL's, not the host
+                mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
+            y = self.gen.finalize(mom, M, flags, ws)
         if slot is not None:  # prepare() may refill this workspace once the finalize has run
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.gen.device))
@@ -175,6 +181,11 @@ class ShardedLabeler:
         m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
+        if self.world == 1:  # one rank: the labels come out of the moments' reduce launch
+            y, _ = self.gen.label_moments_finalize(tx, point_base, M, flags, ws)
+            if on_moments_end:
+                on_moments_end()
+            return y
         mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags, ws)
         if on_moments_end:
             on_moments_end()

@@ -175,6 +175,13 @@ int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M,
                       uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, void* ws,
                       size_t ws_bytes, void* stream);
 
+/* dpi_label_moments over all of [0, M) with the labels finalized by the same block-reduce launch
+ * (y as dpi_label_finalize): one launch less for a single-rank caller.  flags may include
+ * DPI_PREPARED. */
+int dpi_label_moments_finalize(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                               uint32_t epoch, uint32_t point_base, int flags, float sample_bound, float* y,
+                               float* moments, void* ws, size_t ws_bytes, void* stream);
+
 /* parts: (n_parts, n, 2, 1+nx) -> out (n, 2, 1+nx) with the same pairwise tree as
  * dpi_label_moments' block sum.  `parts` is read only. */
 int dpi_moments_reduce(float* parts, int n_parts, int n, int nx, float* out, void* stream);

@@ -62,6 +62,11 @@ class OracleGen:
         y[:, 0] += self.gx
         return torch.from_numpy(y)
 
+    def label_moments_finalize(self, tx, point_base, M_, flags, ws):
+        """The single-rank call (dpi_label_moments_finalize): all of [0, M), finalized."""
+        mom = self.label_moments(tx, point_base, M_, 0, M_, flags, ws)
+        return self.finalize(mom, M_, flags, ws), mom
+
 
 class OracleGenTwoPhase(OracleGen):
     """For begin()/end(): g(x) per batch is recomputed at finalize (the device path keeps it in the
