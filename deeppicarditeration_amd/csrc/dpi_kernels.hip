@@ -811,6 +811,17 @@ static void gemm(int epi, int M, int N, int K, const float* A, int lda, const fl
     hipLaunchKernelGGL(k_gemm_nt<EPI_DELU>, grid, block, 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux);
 }
 
+static int cu_count() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    ncu = std::max(1, ncu);
+  }
+  return ncu;
+}
+
 // Split-storage GEMM: OUT (M x Np) = epi(X (M x Kp) W^T), all split (Np, Kp multiples of 32).
 template <int NT>
 static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
@@ -847,8 +858,7 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   const int ld = L.stride, NXK = (pd.nx + 31) & ~31, NOP = r64(pd.nx);
   // t_encoder -> IN[:, 0:64] and smooth -> SC + 5 in one launch (one block per CU: 144 KB of weights in LDS)
   if (R > 0) {
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int ncu = cu_count();
     const int blocks = std::max(1, std::min(ncu, (R + 16 * (PT_THREADS / 64) - 1) / (16 * (PT_THREADS / 64))));
     hipLaunchKernelGGL(k_pis_time<4>, dim3(blocks), dim3(PT_THREADS), 0, st, pd, rows, L, R);
   }
@@ -1032,9 +1042,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       // previous batch's GEMM blocks instead of packing whole CUs (which starves the GEMM)
       int step = g;
       if (prepare_only) {
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        step = std::max(1, ncu);
+        step = cu_count();
       }
       for (int bx0 = 0; bx0 < g; bx0 += step)
         hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,

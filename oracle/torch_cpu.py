@@ -1,9 +1,12 @@
 """CPU baseline for bench.py (test / measurement infrastructure, never on the product path): the
 reference's own label algorithm, vectorised in PyTorch on the host cores, as the reference runs it
 on a CPU — `estimate_terminal_with_gradients` (picard/data.py:899-926) + `estimate_integral_with_
-gradients` (:471-527) with `get_f` (:1226-1325) for equations whose nonlinearity is ff(t, x, u, grad u)
-(Cha, OUProcessEquation): one Gaussian jump per path (the reference's sampler, equations.py:217-230),
-u and grad u of the network by autograd, the per-point baseline f(t, x) evaluated once and repeated.
+gradients` (:471-527) with `get_f` (:1226-1325): for ff(t, x, u, grad u) equations (Cha,
+OUProcessEquation) u and grad u of the network by autograd; for the Hessian-term equation
+(GBMEquationComplexExact) the SDGD branch of get_f (:1273-1303) — per path v indices drawn with
+randint (:501), one autograd pass per index for u_ii, the baseline's whole diagonal (arange indices)
+gathered per path.  One Gaussian jump per path (the reference's sampler, equations.py:217-230), the
+per-point baseline f(t, x) evaluated once and repeated.
 
 The equations and networks are the torch modules of deeppicarditeration_amd (the plugin interface),
 evaluated on the CPU in fp32 or fp64; the noise is torch's CPU generator (as in the reference).
@@ -52,10 +55,27 @@ def _u_grad(net, s, X):
     return u.detach(), g[:, 1:]
 
 
-def labels_reference_algorithm(eq, net, tx, M, gen, noise=None):
+def _u_grad_sdgd(net, s, X, idx):
+    """u, grad u and u_ii at the columns idx (R, v) (get_f's SDGD loop, data.py:1273-1294; one
+    autograd pass per index with create_graph as there)."""
+    X = X.detach().requires_grad_(True)
+    with torch.enable_grad():
+        u = net(torch.cat([s, X], -1))
+        (ux,) = torch.autograd.grad(u.sum(), X, create_graph=True, retain_graph=True)
+        uii = torch.zeros(idx.shape, dtype=X.dtype)
+        for i in range(idx.shape[1]):
+            ai = idx[:, i:i + 1]
+            (h,) = torch.autograd.grad(torch.gather(ux, 1, ai), X, grad_outputs=torch.ones_like(ai, dtype=X.dtype),
+                                       create_graph=True, retain_graph=True)
+            uii[:, i] = torch.gather(h, 1, ai).squeeze(1).detach()
+    return u.detach(), ux.detach(), uii
+
+
+def labels_reference_algorithm(eq, net, tx, M, gen, noise=None, v=None):
     """(n, 1+nx) labels for points tx (n, 1+nx), M paths each, in tx's dtype.  `noise` = (xi (R, nx),
-    U (R, 1), zeta (R, nx)), R = n M, replaces the three path draws (tests pin the algorithm
-    against the reference's golden outputs this way)."""
+    U (R, 1), zeta (R, nx)[, SDGD indices (R, v)]), R = n M, replaces the path draws (tests pin the
+    algorithm against the reference's golden outputs this way).  v: SDGD samples per path for a
+    Hessian-term equation (default nx)."""
     n, nx = tx.shape[0], eq.nx
     dt = tx.dtype
     T = float(eq.T)
@@ -76,16 +96,26 @@ def labels_reference_algorithm(eq, net, tx, M, gen, noise=None):
     zeta = torch.randn(n * M, nx, generator=gen, dtype=dt) if noise is None else noise[2]
     sig = torch.sqrt(s - t)
     Xs = x + sig * a * zeta
-    u, ux = _u_grad(net, s, Xs)
-    f = eq.ff(s, Xs, u, ux)
-    ub, uxb = _u_grad(net, tx[:, :1], tx[:, 1:])  # baseline once per point (get_f baseline_repeat)
-    fb = eq.ff(tx[:, :1], tx[:, 1:], ub, uxb).repeat_interleave(M, 0)
+    if getattr(eq, "has_hessian_term", False):
+        v = nx if v is None else v
+        idx = torch.randint(0, nx, (n * M, v), generator=gen) if noise is None else noise[3]
+        u, _, uii = _u_grad_sdgd(net, s, Xs, idx)
+        f = eq.ffi(s, Xs, u, uii)
+        # baseline (get_f with baseline_repeat, :1279-1302): the whole diagonal once per point,
+        # repeated and gathered at each path's indices
+        ub, _, uiib = _u_grad_sdgd(net, tx[:, :1], tx[:, 1:], torch.arange(nx).repeat(n, 1))
+        fb = eq.ffi(t, x, ub.repeat_interleave(M, 0), torch.gather(uiib.repeat_interleave(M, 0), 1, idx))
+    else:
+        u, ux = _u_grad(net, s, Xs)
+        f = eq.ff(s, Xs, u, ux)
+        ub, uxb = _u_grad(net, tx[:, :1], tx[:, 1:])  # baseline once per point (get_f baseline_repeat)
+        fb = eq.ff(tx[:, :1], tx[:, 1:], ub, uxb).repeat_interleave(M, 0)
     c = (T - t) * (f - fb) * torch.cat([ones, zeta / sig / a], -1)
     c[:, :1] += fb * (T - t)
     return y + c.view(n, M, 1 + nx).mean(1)
 
 
-def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, points_per_call=4, threads=None):
+def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, points_per_call=4, threads=None, v=None):
     """path-labels/s of labels_reference_algorithm on `threads` host threads for ~target_s seconds."""
     threads = threads or host_cores()
     prev = torch.get_num_threads()
@@ -94,12 +124,12 @@ def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, poi
     gen = torch.Generator().manual_seed(0)
     done = calls = 0
     try:
-        labels_reference_algorithm(eq, net, sample_points(points_per_call, 0).to(dtype), M, gen)  # warm-up
+        labels_reference_algorithm(eq, net, sample_points(points_per_call, 0).to(dtype), M, gen, v=v)  # warm-up
         t0 = time.perf_counter()
         while True:
             tx = sample_points(points_per_call, calls * points_per_call).to(dtype)
             # (no finiteness check: in fp32 the reference's s - t rounds to 0 for tiny U, giving inf)
-            labels_reference_algorithm(eq, net, tx, M, gen)
+            labels_reference_algorithm(eq, net, tx, M, gen, v=v)
             done += points_per_call * M
             calls += 1
             dt = time.perf_counter() - t0

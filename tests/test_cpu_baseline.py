@@ -14,7 +14,8 @@ from oracle import philox as px
 from oracle import torch_cpu as TC
 
 
-@pytest.mark.parametrize("name", ["cha_mlp16_K4", "cha_mlp64x3_K50", "ou_mlp16_K2", "ou_pis32_K2", "cha_zero_K2"])
+@pytest.mark.parametrize("name", ["cha_mlp16_K4", "cha_mlp64x3_K50", "ou_mlp16_K2", "ou_pis32_K2", "cha_zero_K2",
+                                  "gbm_mlp16_sdgd_K2"])
 def test_torch_cpu_baseline_matches_reference_fixture(name):
     f = load(name)
     eq = product_equation(f)
@@ -29,7 +30,11 @@ def test_torch_cpu_baseline_matches_reference_fixture(name):
     U = px.uniforms(px.TAG_S, epoch, seed, ii, mm, open_low=True).reshape(n * M, 1)
     noise = [torch.from_numpy(a) for a in ((S_T / math.sqrt(K)).reshape(n * M, eq.nx), U,
                                            (S_s / math.sqrt(K)).reshape(n * M, eq.nx))]
-    y = TC.labels_reference_algorithm(eq, net, torch.from_numpy(f["tx"]), M, None, noise=noise)
+    v = int(f.get("v", 0))
+    if v > 0:  # SDGD indices (make_golden.py draw 7)
+        noise.append(torch.from_numpy(px.randint_idx(px.TAG_SDGD, epoch, seed, ii, mm, v, eq.nx).reshape(n * M, v)
+                                      .astype(np.int64)))
+    y = TC.labels_reference_algorithm(eq, net, torch.from_numpy(f["tx"]), M, None, noise=noise, v=v or None)
     ref = f["y"]
     assert np.linalg.norm(y.detach().numpy() - ref) / np.linalg.norm(ref) < 1e-11
 
