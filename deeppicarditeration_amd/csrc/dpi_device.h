@@ -1173,21 +1173,24 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
     // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
     __shared__ float lamb[4][HMAX];
+    __shared__ float cb[HMAX];
     __shared__ float ztb[2][64][NXP_MAX];
     if (tid < H) lamb[L - 1][tid] = net.wout[tid];
     __syncthreads();
+    // adjoints: lam_l = W_{l+1}^T (elu'(a_{l+1}) * lam_{l+1}), a k-sliced mat-vec over the block with
+    // every weight load in flight (W_{l+1} row-major (H_out, H_in) is its transposed operand)
     for (int l = L - 2; l >= 0; --l) {
-      if (tid < H) {
-        const float* w = net.W[l + 1];
-        float acc = 0.f;
-        for (int h = 0; h < H; ++h) acc = fmaf(w[(size_t)h * H + tid], delu_from_a(act[l + 1][h]) * lamb[l + 1][h], acc);
-        lamb[l][tid] = acc;
-      }
+      if (tid < H) cb[tid] = delu_from_a(act[l + 1][tid]) * lamb[l + 1][tid];
+      __syncthreads();
+      const float acc = matvec(net.W[l + 1], cb, H);
+      if (tid < H) lamb[l][tid] = acc;
       __syncthreads();
     }
     // Tangent sweep as an LDS mat-mat per layer: thread (d = tid % 128, hg = tid / 128) owns the
-    // rows h = hg, hg + 8, ... of the tangent Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k]) Z_{l-1}[k][d].
-    __shared__ float wsc[64 * 65];
+    // rows h = hg + 8 j of the tangent Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k]) Z_{l-1}[k][d];
+    // k runs outermost in steps of 4, so one Z read serves all 8 rows and each row's 4 scaled
+    // weights come in one broadcast ds_read_b128 (every output is the same k-ascending fma chain).
+    __shared__ __attribute__((aligned(16))) float wsc[64 * 64];
     __shared__ float udp[8][NXP_MAX];
     const int d = tid % NXP_MAX, hg = tid / NXP_MAX;  // NTHB = 8 x NXP_MAX
     float ud = 0.f;
@@ -1197,17 +1200,38 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
     }
     int cz = 0;
+    const int H4 = H & ~3;
     for (int l = 1; l < L; ++l) {
       for (int q = tid; q < H * H; q += NTHB) {
         const int h = q / H, k = q - h * H;
-        wsc[h * 65 + k] = net.W[l][q] * delu_from_a(act[l - 1][k]);
+        wsc[h * 64 + k] = net.W[l][q] * delu_from_a(act[l - 1][k]);
       }
       __syncthreads();  // wsc and Z_{l-1} complete
-      for (int h = hg; h < H; h += 8) {
-        float z = 0.f;
-        for (int k = 0; k < H; ++k) z = fmaf(wsc[h * 65 + k], ztb[cz][k][d], z);
-        ztb[cz ^ 1][h][d] = z;
-        ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z * z, ud);
+      float z[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = 0.f;
+      for (int k = 0; k < H4; k += 4) {
+        const float z0 = ztb[cz][k][d], z1 = ztb[cz][k + 1][d], z2 = ztb[cz][k + 2][d], z3 = ztb[cz][k + 3][d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (hg + 8 * j < H) {
+            const float4 w = *reinterpret_cast<const float4*>(&wsc[(hg + 8 * j) * 64 + k]);
+            z[j] = fmaf(w.w, z3, fmaf(w.z, z2, fmaf(w.y, z1, fmaf(w.x, z0, z[j]))));
+          }
+      }
+      for (int k = H4; k < H; ++k) {
+        const float zk = ztb[cz][k][d];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (hg + 8 * j < H) z[j] = fmaf(wsc[(hg + 8 * j) * 64 + k], zk, z[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int h = hg + 8 * j;
+        if (h < H) {
+          ztb[cz ^ 1][h][d] = z[j];
+          ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z[j] * z[j], ud);
+        }
       }
       cz ^= 1;
       __syncthreads();  // before wsc is overwritten
