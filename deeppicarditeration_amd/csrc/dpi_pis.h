@@ -129,6 +129,7 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
   for (int j = wv; do_term && j < nb; j += 4) {  // terminal path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (TERM)
+#pragma unroll 2
       for (int k = 0; k < K; ++k) {
         const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3t, k0, k1));
         s0 += z.a;
@@ -153,6 +154,7 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
   for (int j = 3 - wv; do_int && j < nb; j += 4) {  // integral path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (INTG)
+#pragma unroll 2
       for (int k = 0; k < K; ++k) {
         const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3i, k0, k1));
         s0 += z.a;
