@@ -1482,6 +1482,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   constexpr bool GBM = KIND == DPI_EQ_GBM;
+  // two independent Philox chains per wave in the noise loops (2 % on the one- and two-wave-per-SIMD
+  // kernels); the Hessian-label kernel's register allocation measured 4 % slower with it
+  constexpr int NOISE_UNROLL = HESS ? 1 : 2;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1594,6 +1597,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
       if (TERM && j < nb) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        #pragma unroll NOISE_UNROLL
         for (int k = 0; k < a.K; ++k) {
           const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
           s0 += z.a;
@@ -1620,6 +1624,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       if (j < nb) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         if (INTG) {
+          #pragma unroll NOISE_UNROLL
           for (int k = 0; k < a.K; ++k) {
             const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
             s0 += z.a;
