@@ -243,7 +243,7 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
                                         const uint32_t* __restrict__ W, float wscale, const float* __restrict__ X,
                                         int ldx, const float* __restrict__ X2, int ldx2, int nk1,
                                         float* __restrict__ OUT, int ldc, const float* __restrict__ bias,
-                                        const float* __restrict__ AUX, int ldaux) {
+                                        const float* __restrict__ AUX, int ldaux, int stage_aux = 1) {
   static_assert(NT == 2 || NT == 4, "wave n-tiles");
   constexpr int BN = 32 * NT, BM = X3_BM, STAGE = (BN + BM) * 32, NWAVE = X3_THREADS / 64;
   constexpr int NINS = (BN + BM) / 8, PER_WAVE = NINS / NWAVE;  // DMA wave-instructions per chunk
@@ -275,6 +275,29 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
         src = xb + (size_t)min(m0 + r - BN, M - 1) * ld + 4 * g;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+    }
+  };
+  // DELU epilogue operand staging (NT = 4, nk >= 3): the two DMA slots that the last two load
+  // steps would refill with clamped duplicates of the last chunk take this tile's saved activations
+  // instead — per wave its 64 rows x 2 output chunks (256 B per row), rows 0-23 in the slot freed at
+  // step nk - 3 and rows 24-47 in the slot freed at step nk - 2 (6 DMA instructions per wave each, as
+  // many as the duplicates they replace, so every counted wait stays exact); rows 48-63 go straight
+  // to registers after the last MFMAs and land while rows 0-47 are processed.  Row rho's 16 granules
+  // sit at position g ^ (rho & 15): the epilogue's ds_read_b128 lane groups hit 16 distinct slots.
+  constexpr bool AUXC = EPI == EPI_DELU && NT == 4 && PER_WAVE == 6;
+  const bool aux_lds = AUXC && nk >= 3 && stage_aux;
+  auto issue_aux = [&](int part, int slot) {
+    uint32_t* dst = sm + slot * STAGE + wv * 1536;
+    const int U0 = (n0 >> 5) + wn * 2;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      int rho = 24 * part + 4 * k + (lane >> 4);
+      asm volatile("" : "+v"(rho));  // computed here, not hoisted out of the K loop
+      const int gs = (lane & 15) ^ (rho & 15);
+      const int mrow = min(m0 + wm * 64 + rho, M - 1);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(AUX) + (size_t)mrow * ldaux + 32 * U0 + 4 * gs;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + 256 * k), 16, 0, 0);
     }
   };
   auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {
@@ -321,7 +344,10 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): chunk u's reads landed (visible to the compiler)
     vm_wait();                           // own DMA of chunk u + 1 landed
     __builtin_amdgcn_s_barrier();        // chunk u + 1 published; chunk u's slot free
-    issue(min(u + 3, nk - 1), u % X3_STAGES);
+    if (AUXC && aux_lds && u + 3 >= nk)
+      issue_aux(u + 3 - nk, u % X3_STAGES);
+    else
+      issue(min(u + 3, nk - 1), u % X3_STAGES);
     load((u + 1) % X3_STAGES, std::integral_constant<int, F ^ 1>{});
     mma(Fc);
     constexpr int NRD = 2 * (NT + 4), NMF = 3 * NT * 4;  // ds_reads and MFMAs per chunk
@@ -374,7 +400,21 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
     __builtin_amdgcn_s_waitcnt(0xC07F);
     mma(std::integral_constant<int, 0>{});
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail DMAs land before the slot memory is released
+  u32x4_t a3h[2], a3l[2];  // staged DELU epilogue: saved activations of rows 48-63
+  if (AUXC && aux_lds) {
+    asm volatile("" ::: "memory");  // these loads stay after the staging DMAs
+    const int mrow = min(m0 + wm * 64 + 48 + il, M - 1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const u32x4_t* g = reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint32_t*>(AUX) + (size_t)mrow * ldaux +
+                                                        32 * ((n0 >> 5) + wn * 2 + c) + 8 * ql);
+      a3h[c] = g[0];
+      a3l[c] = g[1];
+    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // this wave's staged rows 0-47 landed
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail DMAs land before the slot memory is released
+  }
 
   // epilogue: lane (il, ql) of m-tile b holds OUT[m = m0 + 64 wm + 16 b + il][n = 16 T + 4 ql + r]
   // for the wave's n-tiles T; tiles (2c, 2c+1) form granule pair ql of output chunk U.
@@ -403,7 +443,23 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
       } else {
         float a[8];
-        x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+        if (AUXC && aux_lds) {
+          u32x4_t h, l;
+          if (b < 3) {  // staged in LDS: row rho of part rho / 24
+            const int rho = 16 * b + il, part = rho >= 24 ? 1 : 0;
+            const uint32_t* rb = sm + ((nk - 3 + part) % X3_STAGES) * STAGE + wv * 1536 + 64 * (rho - 24 * part);
+            const int gh = 8 * c + 2 * ql;
+            h = *reinterpret_cast<const u32x4_t*>(rb + 4 * (gh ^ (rho & 15)));
+            l = *reinterpret_cast<const u32x4_t*>(rb + 4 * ((gh + 1) ^ (rho & 15)));
+          } else {
+            h = a3h[c];
+            l = a3l[c];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) a[j] = x3_join(h[j >> 1], l[j >> 1], j & 1);
+        } else {
+          x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
       }
@@ -418,11 +474,11 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
                                                            const float* __restrict__ X2, int ldx2, int nk1,
                                                            float* __restrict__ OUT, int ldc,
                                                            const float* __restrict__ bias,
-                                                           const float* __restrict__ AUX, int ldaux) {
+                                                           const float* __restrict__ AUX, int ldaux, int stage_aux) {
   __shared__ X3Lds<NT> lds;
   const int tile = x3_tile_of_block(), mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
   x3_tile<EPI, NT, VAR>(lds.sm, mt * X3_BM, nt * 32 * NT, M, Kp, W, wscale, X, ldx, X2, ldx2, nk1, OUT, ldc, bias, AUX,
-                        ldaux);
+                        ldaux, stage_aux);
 }
 
 

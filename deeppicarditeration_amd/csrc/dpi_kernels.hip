@@ -822,6 +822,17 @@ static int cu_count() {
   return ncu;
 }
 
+// DELU epilogue operands staged through the ring's last two DMA slots (k_gemm_x3); DPI_X3_STAGE=0
+// loads them in the epilogue instead (ablation).
+static int x3_stage_aux() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_X3_STAGE");
+    v = e ? (std::atoi(e) != 0) : 1;
+  }
+  return v;
+}
+
 // Split-storage GEMM: OUT (M x Np) = epi(X (M x Kp) W^T), all split (Np, Kp multiples of 32).
 template <int NT>
 static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
@@ -831,13 +842,13 @@ static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float 
   dim3 grid(nnt * nmt), block(X3_THREADS);
   if (epi == EPI_BIAS)
     hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
-                       ldc, bias, aux, ldaux);
+                       ldc, bias, aux, ldaux, 0);
   else if (epi == EPI_BIAS_ELU)
     hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1,
-                       OUT, ldc, bias, aux, ldaux);
+                       OUT, ldc, bias, aux, ldaux, 0);
   else
     hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
-                       ldc, bias, aux, ldaux);
+                       ldc, bias, aux, ldaux, x3_stage_aux());
 }
 // ws: the weight matrix's scale 2^-s (pack_split_x3).  X2 != nullptr: K columns [k1, Kp) come from X2.
 static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx, float* OUT,

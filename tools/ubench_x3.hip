@@ -327,6 +327,8 @@ __global__ void k_fill(float* rows, int M, int Kp, int ld, uint32_t seed, float 
   }
 }
 
+static int g_stage = 1;  // DELU epilogue operands staged through the ring (k_gemm_x3 stage_aux)
+
 struct Bufs {
   int M, Kp, Np;
   uint32_t* W;
@@ -348,7 +350,7 @@ static void launch(const Bufs& b, float* out) {
     const int nnt = b.Np / 128, nmt = (b.M + X3_BM - 1) / X3_BM;
     hipLaunchKernelGGL((k_gemm_x3<EPI, 4, VAR>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, b.M, b.Kp, nnt, b.W,
                        1.0f / 16.0f, b.X, b.Kp, b.X, b.Kp, b.Kp / 32, out, b.Np, EPI == EPI_DELU ? nullptr : b.bias,
-                       b.AUX, b.Np);
+                       b.AUX, b.Np, g_stage);
   }
 }
 
@@ -513,6 +515,20 @@ int main(int argc, char** argv) {
       launch<EPI_DELU, 0>(b, b.REF);
       run<EPI_DELU, 0>("product", b, iters);
       run<EPI_DELU, 100>("k_gemm_x4 256x256, 1 wave/SIMD", b, iters);
+    }
+    return 0;
+  }
+  if (argc > 3 && std::strcmp(argv[3], "stage") == 0) {  // DELU: staged epilogue operands vs epilogue loads
+    for (int kp : {512, 128}) {
+      b.Kp = kp;
+      for (int rep = 0; rep < 2; ++rep) {
+        g_stage = 0;
+        launch<EPI_DELU, 0>(b, b.REF);
+        run<EPI_DELU, 0>(kp == 512 ? "K 512 epilogue loads" : "K 128 epilogue loads", b, iters);
+        g_stage = 1;
+        CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
+        run<EPI_DELU, 0>(kp == 512 ? "K 512 staged" : "K 128 staged", b, iters);
+      }
     }
     return 0;
   }
