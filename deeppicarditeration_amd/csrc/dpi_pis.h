@@ -635,28 +635,47 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
   const float yT = 1.0f / (sqrtf(Kf * tmt) * e.asq), yI = 1.0f / (sqrtf(Kf * smt) * e.asq);
-  // this row's contributions: v[2k + mom] for dim d = q + 4k (k < 32: nx <= 128), the value column
-  // (lane group q = 0) apart
+  // this row's contributions: v[2k + mom] for dim d = 16 (k >> 2) + 4 q + (k & 3) (k < 32: nx <= 128),
+  // the value column (lane group q = 0) apart.  The noise sums come in 16-B loads: the 4 lanes of a
+  // row read 64 contiguous bytes per instruction (8 + 8 loads per lane instead of 32 + 32 single floats)
   static_assert(NXP_MAX <= 128, "dims per lane group");
   float v[64];
   const float aY = ap * yT, bY = bp * yI;
 #pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    const int d = q + 4 * k;
-    const float c = d < nx ? fmaf(aY, row[L.ST + d], bY * row[L.SS + d]) : 0.f;
-    v[2 * k] = c;
-    v[2 * k + 1] = c * c;
+  for (int kk = 0; kk < 8; ++kk) {
+    const int d0 = 16 * kk + 4 * q;
+    float4 st4 = make_float4(0.f, 0.f, 0.f, 0.f), ss4 = st4;
+    if (d0 < nx) {  // the regions hold round_up(nx, 4) floats: a quad never leaves its region
+      st4 = *reinterpret_cast<const float4*>(row + L.ST + d0);
+      ss4 = *reinterpret_cast<const float4*>(row + L.SS + d0);
+    }
+    const float sts[4] = {st4.x, st4.y, st4.z, st4.w}, sss[4] = {ss4.x, ss4.y, ss4.z, ss4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 4 * kk + j;
+      const float c = d0 + j < nx ? fmaf(aY, sts[j], bY * sss[j]) : 0.f;
+      v[2 * k] = c;
+      v[2 * k + 1] = c * c;
+    }
   }
   float c0 = q == 0 ? ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f) : 0.f, c0s = c0 * c0;
   // sum over the wave's 16 rows (lane = 4 row + q) by a halving butterfly on lane bits 5..2: at bit
   // m a lane keeps the half of its values selected by that bit and adds its partner's copy, so lane
-  // (row r, q) ends with values 4r .. 4r + 3 summed over the 16 rows of lane group q
+  // (row r, q) ends with values 4r .. 4r + 3 summed over the 16 rows of lane group q.  Bits 5 and 4
+  // (48 of the 60 exchanges) are the gfx950 VALU lane swaps (v_permlane32/16_swap, no LDS
+  // crossbar); every sum is the same pair of operands as an xor exchange, so bitwise unchanged.
   const int lane = tid & 63, wv = tid >> 6;
+  c0 = qsum(c0);  // the value column over the same lane bits (5, 4 here; 3, 2 below)
+  c0s = qsum(c0s);
 #pragma unroll
-  for (int bit = 5; bit >= 2; --bit) {  // the value column: a plain xor tree over the same lane bits
+  for (int bit = 3; bit >= 2; --bit) {
     c0 += __shfl_xor(c0, 1 << bit, 64);
     c0s += __shfl_xor(c0s, 1 << bit, 64);
   }
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = swap32_sum(v[j], v[j + 32]);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = swap16_sum(v[j], v[j + 16]);
 #define DPI_HALVE(BIT, H)                                          \
   _Pragma("unroll") for (int j = 0; j < H; ++j) {                  \
     const bool up = (lane >> BIT) & 1;                             \
@@ -664,8 +683,6 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
     const float send = up ? v[j] : v[j + H];                       \
     v[j] = keep + __shfl_xor(send, 1 << BIT, 64);                  \
   }
-  DPI_HALVE(5, 32)
-  DPI_HALVE(4, 16)
   DPI_HALVE(3, 8)
   DPI_HALVE(2, 4)
 #undef DPI_HALVE
@@ -679,9 +696,9 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   // the four waves' sums, (w0 + w1) + (w2 + w3): a fixed order independent of rank and chunk
   float* out = partial + ((size_t)i * nbp + b) * slab_row(F);  // [point][block][slab_row(F)]
   {
-    const int qq = tid >> 6, j = tid & 63, k = j >> 1, mom = j & 1;
+    const int qq = tid >> 6, j = tid & 63, k = j >> 1, mom = j & 1, d = 16 * (k >> 2) + 4 * qq + (k & 3);
     const float sum = (part[0][qq][j] + part[1][qq][j]) + (part[2][qq][j] + part[3][qq][j]);
-    if (qq + 4 * k < nx) out[mom * F + 1 + qq + 4 * k] = sum;
+    if (d < nx) out[mom * F + 1 + d] = sum;
     if (tid < 2) out[tid * F] = (vsum[0][tid] + vsum[1][tid]) + (vsum[2][tid] + vsum[3][tid]);
   }
 }
