@@ -519,17 +519,27 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "stage") == 0) {  // DELU: staged epilogue operands vs epilogue loads
-    for (int kp : {512, 128}) {
+    // K 512 / 128 are the HJB chain's; 96 and 160 (odd chunk counts) and a partial last m-tile
+    // (M % 256 != 0) cover the staging's other branches
+    const int M0 = b.M;
+    for (int kp : {512, 128, 96, 160}) {
       b.Kp = kp;
-      for (int rep = 0; rep < 2; ++rep) {
-        g_stage = 0;
-        launch<EPI_DELU, 0>(b, b.REF);
-        run<EPI_DELU, 0>(kp == 512 ? "K 512 epilogue loads" : "K 128 epilogue loads", b, iters);
-        g_stage = 1;
-        CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
-        run<EPI_DELU, 0>(kp == 512 ? "K 512 staged" : "K 128 staged", b, iters);
+      for (int m : {M0, M0 - 192}) {
+        b.M = m;
+        for (int rep = 0; rep < (kp >= 128 && m == M0 ? 2 : 1); ++rep) {
+          char n0[64], n1[64];
+          std::snprintf(n0, sizeof n0, "K %d M %d epilogue loads", kp, m);
+          std::snprintf(n1, sizeof n1, "K %d M %d staged", kp, m);
+          g_stage = 0;
+          launch<EPI_DELU, 0>(b, b.REF);
+          run<EPI_DELU, 0>(n0, b, iters);
+          g_stage = 1;
+          CK(hipMemset(b.OUT, 0, (size_t)M0 * b.Np * 4));
+          run<EPI_DELU, 0>(n1, b, iters);
+        }
       }
     }
+    b.M = M0;
     return 0;
   }
   if (argc > 3 && std::strcmp(argv[3], "prod") == 0) {  // profiling: the product kernels only
