@@ -233,7 +233,7 @@ __device__ __forceinline__ int x3_tile_of_block() {
 template <int NT>
 struct X3Lds {
   static constexpr int BN = 32 * NT, STAGE = (BN + X3_BM) * 32;
-  uint32_t sm[X3_STAGES * STAGE];
+  uint32_t sm[X3_STAGES * STAGE + BN];  // the ring, then the block's n-tile of the bias
 };
 
 // One 256 x BN output tile (rows m0.., units n0..) of the split GEMM, the whole K loop and the
@@ -377,6 +377,14 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
   // above any co-resident wave of another kernel (the prepare stream's rollout): the
   // GEMM's issue comes first, the VALU-bound rollout takes the cycles the GEMM leaves
   if constexpr (!(VAR & 1)) __builtin_amdgcn_s_setprio(2);
+  // the bias of the block's n-tile goes to LDS with the prologue (older than every DMA, so the
+  // chunk-0 wait covers it): the epilogue then reads it without a global round trip
+  // (VAR bit 3: the epilogue's global bias loads instead — the ablation of tools/ubench_x3.hip)
+  constexpr bool LDS_BIAS = !(VAR & 8);
+  const bool has_bias = (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && bias != nullptr;
+  float* sbias = reinterpret_cast<float*>(sm + X3_STAGES * STAGE);
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (LDS_BIAS && has_bias && tid < BN / 4) bv = *reinterpret_cast<const float4*>(bias + n0 + 4 * tid);
   // prologue: chunks 0, 1, 2 (clamped) in flight; publish chunk 0 and read it
   issue(0, 0);
   issue(min(1, nk - 1), 1);
@@ -385,6 +393,7 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
     asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  if (LDS_BIAS && has_bias && tid < BN / 4) *reinterpret_cast<float4*>(sbias + 4 * tid) = bv;
   __builtin_amdgcn_s_barrier();
   load(0, std::integral_constant<int, 0>{});
   int u = 0;
@@ -432,9 +441,11 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
         v[4 + r] = acc[2 * c + 1][b][r] * wscale;
       }
       if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
-        if (bias) {
-          const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
-          const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 16 + 4 * ql);
+        if (has_bias) {
+          const int o = 32 * (wn * (NT / 2) + c) + 4 * ql;  // = 32 U + 4 ql - n0
+          const float* bsrc = LDS_BIAS ? sbias + o : bias + 32 * U + 4 * ql;
+          const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+          const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
           v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
           v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
         }

@@ -518,6 +518,15 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "bias") == 0) {  // ELU: bias staged in LDS (product) vs epilogue loads (VAR 8)
+    for (int rep = 0; rep < 3; ++rep) {
+      launch<EPI_BIAS_ELU, 0>(b, b.REF);
+      run<EPI_BIAS_ELU, 8>("ELU bias: epilogue global loads", b, iters);
+      CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
+      run<EPI_BIAS_ELU, 0>("ELU bias: staged in LDS", b, iters);
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "stage") == 0) {  // DELU: staged epilogue operands vs epilogue loads
     // K 512 / 128 are the HJB chain's; 96 and 160 (odd chunk counts) and a partial last m-tile
     // (M % 256 != 0) cover the staging's other branches
