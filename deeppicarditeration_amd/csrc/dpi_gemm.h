@@ -224,10 +224,13 @@ constexpr int X3_BM = 256, X3_STAGES = 3, X3_THREADS = 512;
 // with the first MFMAs.
 // XCD-aware bijective remap (dispatch puts block b on XCD b % 8): the n-tiles of one m-tile run
 // back to back on one XCD
+// The nwg % 8 blocks past 8 (nwg / 8) — dispatched last — take the LAST tiles, i.e. the chunk's
+// partial m-tile (its n-tiles are the launch's final round, cheap with dead waves skipped), instead
+// of giving XCDs 0..r8-1 one full tile more than the others.
 __device__ __forceinline__ int x3_tile_of_block() {
   const int nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int q8 = nwg >> 3;
+  return loc < q8 ? xcd * q8 + loc : 8 * q8 + xcd;
 }
 
 template <int NT>
@@ -395,6 +398,22 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   if (LDS_BIAS && has_bias && tid < BN / 4) *reinterpret_cast<float4*>(sbias + 4 * tid) = bv;
   __builtin_amdgcn_s_barrier();
+  if (m0 + wm * 64 >= M) {
+    // every row of this wave lies past M (the chunk's partial last m-tile): no MFMAs, fragment reads
+    // or stores — its share of each chunk's DMA (the same instructions the live waves' loop issues,
+    // so the staged epilogue regions stay intact) and the same barriers, then done; the wave's SIMD
+    // partner runs its MFMAs alone
+    for (int u = 0; u + 1 < nk; ++u) {
+      vm_wait();
+      __builtin_amdgcn_s_barrier();
+      if (AUXC && aux_lds && u + 3 >= nk)
+        issue_aux(u + 3 - nk, u % X3_STAGES);
+      else
+        issue(min(u + 3, nk - 1), u % X3_STAGES);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   load(0, std::integral_constant<int, 0>{});
   int u = 0;
   for (; u + 2 < nk; u += 2) {
