@@ -498,6 +498,178 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_gemm_x3h: the same split GEMM on a 128 x 128 block tile with 4 waves (64 x 64 each, the product's
+// wave tile) and a 2-slot ring of 32 KB chunks, so two blocks share a CU (2 x 64.5 KB of LDS, one wave
+// per SIMD each) and one block's prologue and epilogue run under the other's main loop, at 4/3 the
+// L2 -> LDS bytes per MFMA of the 256 x 128 tile.  Per output the same products in the same order:
+// bitwise equal to k_gemm_x3.  (tools/ubench_x3.hip "half" mode.)
+constexpr int X3H_BM = 128, X3H_THREADS = 256;
+struct X3HLds {
+  static constexpr int BN = 128, STAGE = (BN + X3H_BM) * 32;
+  uint32_t sm[2 * STAGE + BN];
+};
+
+template <int EPI>
+__global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3h(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
+                                                             float wscale, const float* __restrict__ X, int ldx,
+                                                             const float* __restrict__ X2, int ldx2, int nk1,
+                                                             float* __restrict__ OUT, int ldc,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ AUX, int ldaux) {
+  constexpr int NT = 4, BN = 128, BM = X3H_BM, STAGE = X3HLds::STAGE, NWAVE = X3H_THREADS / 64;
+  constexpr int PER_WAVE = (BN + BM) / 8 / NWAVE;  // 8 DMA wave-instructions per chunk
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  __shared__ X3HLds lds;
+  uint32_t* sm = lds.sm;
+  const int tile = x3_tile_of_block(), mt = tile / n_ntiles, ntl = tile - mt * n_ntiles;
+  const int m0 = mt * BM, n0 = ntl * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int il = lane & 15, ql = lane >> 4;
+  const int nk = Kp >> 5;
+  const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
+  const uint32_t* X2w = reinterpret_cast<const uint32_t*>(X2);
+  auto issue = [&](int c, int slot) {
+    uint32_t* dst = sm + slot * STAGE;
+    const bool one = c < nk1;  // two-source K as in x3_tile
+    const uint32_t* xb = one ? Xw + 32 * c : X2w + 32 * (c - nk1);
+    const int ld = one ? ldx : ldx2;
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+      const int w = k * NWAVE + wv;
+      const int r = 8 * w + (lane >> 3);
+      const int g = (lane & 7) ^ x3_swz(r);
+      const uint32_t* src;
+      if (r < BN)
+        src = W + (size_t)(n0 + r) * Kp + 32 * c + 4 * g;
+      else
+        src = xb + (size_t)min(m0 + r - BN, M - 1) * ld + 4 * g;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+    }
+  };
+  auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {
+    const int s = x3_swz(row);
+    const uint32_t* rp = buf + row * 32;
+    h = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql) ^ s)));
+    l = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql + 1) ^ s)));
+  };
+  f4v acc[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[t][b] = f4v{0.f, 0.f, 0.f, 0.f};
+  h8 ah[2][NT], al[2][NT], bh[2][4], bl[2][4];
+  auto load = [&](int slot, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    const uint32_t* buf = sm + slot * STAGE;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) frag(buf, wn * 16 * NT + 16 * t + il, ah[F][t], al[F][t]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) frag(buf, BN + wm * 64 + 16 * b + il, bh[F][b], bl[F][b]);
+  };
+  auto mma = [&](auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bl[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+      }
+  };
+  // iteration u (u + 1 < nk): chunk u in set F; the DMA of chunk u + 1 (issued one iteration ago) is
+  // this wave's only outstanding one; chunk u + 2 goes into chunk u's slot
+  auto body = [&](int u, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < nk) issue(u + 2, u & 1);
+    load((u + 1) & 1, std::integral_constant<int, F ^ 1>{});
+    mma(Fc);
+    constexpr int NRD = 2 * (NT + 4), NMF = 3 * NT * 4;
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF / NRD, 0);
+    }
+  };
+  const bool has_bias = (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && bias != nullptr;
+  float* sbias = reinterpret_cast<float*>(sm + 2 * STAGE);
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (has_bias && tid < BN / 4) bv = *reinterpret_cast<const float4*>(bias + n0 + 4 * tid);
+  __builtin_amdgcn_s_setprio(2);
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (has_bias && tid < BN / 4) *reinterpret_cast<float4*>(sbias + 4 * tid) = bv;
+  __builtin_amdgcn_s_barrier();
+  if (m0 + wm * 64 >= M) {  // rows past M: DMA share and barriers only
+    for (int u = 0; u + 1 < nk; ++u) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (u + 2 < nk) issue(u + 2, u & 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  load(0, std::integral_constant<int, 0>{});
+  int u = 0;
+  for (; u + 2 < nk; u += 2) {
+    body(u, std::integral_constant<int, 0>{});
+    body(u + 1, std::integral_constant<int, 1>{});
+  }
+  if (u + 1 < nk) {
+    body(u, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mma(std::integral_constant<int, 1>{});
+  } else {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mma(std::integral_constant<int, 0>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int m = m0 + wm * 64 + 16 * b + il;
+    if (m >= M) continue;
+#pragma unroll
+    for (int c = 0; c < NT / 2; ++c) {
+      const int U = (n0 >> 5) + wn * (NT / 2) + c;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[2 * c][b][r] * wscale;
+        v[4 + r] = acc[2 * c + 1][b][r] * wscale;
+      }
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
+        if (has_bias) {
+          const float* bsrc = sbias + 32 * (wn * (NT / 2) + c) + 4 * ql;
+          const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+          const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
+          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+        }
+        if (EPI == EPI_BIAS_ELU)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+      } else {
+        float a[8];
+        x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
+      }
+      x3_put8(OUT + (size_t)m * ldc, 0, U, ql, v);
+    }
+  }
+}
+
 template <int EPI, int NT, int VAR = 0>
 __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
                                                            float wscale, const float* __restrict__ X, int ldx,

@@ -833,12 +833,39 @@ static int x3_stage_aux() {
   return v;
 }
 
+// Block tile of the NT = 4 split GEMMs: 128 (default, k_gemm_x3h: two blocks per CU) or 256
+// (DPI_X3_TILE=256: k_gemm_x3, one 8-wave block per CU with the staged DELU epilogue).
+static int x3_tile_rows() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_X3_TILE");
+    v = (e && std::atoi(e) == 256) ? 256 : 128;
+  }
+  return v;
+}
+
 // Split-storage GEMM: OUT (M x Np) = epi(X (M x Kp) W^T), all split (Np, Kp multiples of 32).
 template <int NT>
 static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
                        const float* X2, int ldx2, int k1, float* OUT, int ldc, const float* bias, const float* aux,
                        int ldaux, hipStream_t st) {
   const int nnt = Np / (32 * NT), nmt = (M + X3_BM - 1) / X3_BM, nk1 = k1 / 32;
+  if constexpr (NT == 4) {
+    if (x3_tile_rows() == 128) {
+      const int nmh = (M + X3H_BM - 1) / X3H_BM;
+      dim3 gh(nnt * nmh), bh(X3H_THREADS);
+      if (epi == EPI_BIAS)
+        hipLaunchKernelGGL(k_gemm_x3h<EPI_BIAS>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc, bias,
+                           aux, ldaux);
+      else if (epi == EPI_BIAS_ELU)
+        hipLaunchKernelGGL(k_gemm_x3h<EPI_BIAS_ELU>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc,
+                           bias, aux, ldaux);
+      else
+        hipLaunchKernelGGL(k_gemm_x3h<EPI_DELU>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc, bias,
+                           aux, ldaux);
+      return;
+    }
+  }
   dim3 grid(nnt * nmt), block(X3_THREADS);
   if (epi == EPI_BIAS)
     hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,

@@ -518,6 +518,49 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::strcmp(argv[3], "half") == 0) {  // 128 x 128 tile, two blocks per CU (k_gemm_x3h)
+    for (int rep = 0; rep < 2; ++rep) {
+      for (int e = 0; e < 2; ++e) {
+        const int nnt = b.Np / 128, nmt = (b.M + X3H_BM - 1) / X3H_BM;
+        if (e == 0) {
+          launch<EPI_BIAS_ELU, 0>(b, b.REF);
+          run<EPI_BIAS_ELU, 0>("product 256 x 128", b, iters);
+        } else {
+          launch<EPI_DELU, 0>(b, b.REF);
+          run<EPI_DELU, 0>("product 256 x 128", b, iters);
+        }
+        CK(hipMemset(b.OUT, 0, (size_t)b.M * b.Np * 4));
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        auto go = [&]() {
+          if (e == 0)
+            hipLaunchKernelGGL(k_gemm_x3h<EPI_BIAS_ELU>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, b.M, b.Kp, nnt, b.W,
+                               1.0f / 16.0f, b.X, b.Kp, b.X, b.Kp, b.Kp / 32, b.OUT, b.Np, b.bias, b.AUX, b.Np);
+          else
+            hipLaunchKernelGGL(k_gemm_x3h<EPI_DELU>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, b.M, b.Kp, nnt, b.W,
+                               1.0f / 16.0f, b.X, b.Kp, b.X, b.Kp, b.Kp / 32, b.OUT, b.Np, nullptr, b.AUX, b.Np);
+        };
+        go();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < iters; ++i) go();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        std::vector<uint32_t> a((size_t)b.M * b.Np), r((size_t)b.M * b.Np);
+        CK(hipMemcpy(a.data(), b.OUT, a.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(r.data(), b.REF, r.size() * 4, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < a.size(); ++i) bad += a[i] != r[i];
+        std::printf("%-4s x3h 128 x 128, 2 blocks/CU %26s %8.1f us  differing words %zu\n", e == 0 ? "elu" : "delu", "",
+                    ms * 1e3 / iters, bad);
+        std::fflush(stdout);
+      }
+    }
+    return 0;
+  }
   if (argc > 3 && std::strcmp(argv[3], "bias") == 0) {  // ELU: bias staged in LDS (product) vs epilogue loads (VAR 8)
     for (int rep = 0; rep < 3; ++rep) {
       launch<EPI_BIAS_ELU, 0>(b, b.REF);
