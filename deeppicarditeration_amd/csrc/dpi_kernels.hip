@@ -1053,6 +1053,17 @@ static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, cons
   return 0;
 }
 
+// Independent Philox chains per wave in the PISGradNet rollout: 4 (default; 61 VGPRs) or 2
+// (DPI_PIS_UNROLL=2; 47 VGPRs, room beside the 256 x 128 GEMM's blocks).
+static int pis_rollout_unroll() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_PIS_UNROLL");
+    v = (e && std::atoi(e) == 2) ? 2 : 4;
+  }
+  return v;
+}
+
 // prepared: dpi_label_prepare already ran the first chunk's rollout and baseline rows (same
 // arguments, same workspace); prepare_only: run just those (dpi_label_prepare).
 static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
@@ -1082,10 +1093,16 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       if (prepare_only) {
         step = cu_count();
       }
-      for (int bx0 = 0; bx0 < g; bx0 += step)
-        hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
-                           net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
-                           a.point_base, a.gx, rows, L, stage, dt, bx0);
+      for (int bx0 = 0; bx0 < g; bx0 += step) {
+        if (pis_rollout_unroll() == 4)
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
+                             net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
+                             a.point_base, a.gx, rows, L, stage, dt, bx0);
+        else
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
+                             net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
+                             a.point_base, a.gx, rows, L, stage, dt, bx0);
+      }
     };
     const bool base = g0 == 0;
     float* brows = rows + (size_t)g * P * L.stride;

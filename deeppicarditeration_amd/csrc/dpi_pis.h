@@ -95,7 +95,7 @@ __device__ __forceinline__ void x3_put4(float* row, int reg, int j, const float 
 }
 
 // One (point, 64-path block) of the rollout: bx = the block's index within the chunk.
-template <int KIND, bool X3>
+template <int KIND, bool X3, int UNR = 2>
 __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
                                                   int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                   uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
@@ -129,7 +129,7 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
   for (int j = wv; do_term && j < nb; j += 4) {  // terminal path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (TERM)
-#pragma unroll 2
+#pragma unroll UNR
       for (int k = 0; k < K; ++k) {
         const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3t, k0, k1));
         s0 += z.a;
@@ -154,7 +154,7 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
   for (int j = 3 - wv; do_int && j < nb; j += 4) {  // integral path
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (INTG)
-#pragma unroll 2
+#pragma unroll UNR
       for (int k = 0; k < K; ++k) {
         const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3i, k0, k1));
         s0 += z.a;
@@ -209,11 +209,12 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
   }
 }
 
-// Block bx0 + blockIdx.x of the chunk.  8.7 KB of LDS (no staging of X_s) and 40 VGPRs, so a
-// rollout block (one wave per SIMD) fits on a CU beside a k_gemm_x3 block (144 KB, 2 x 232 VGPRs
-// per SIMD): the prepare stream launches the next batch's rollout in grids of one block per CU.
-template <int KIND, bool X3>
-__global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
+// Block bx0 + blockIdx.x of the chunk.  8.7 KB of LDS (no staging of X_s); UNR independent Philox
+// chains per wave in the noise loops, capped at 64 VGPRs, so a rollout block (one wave per SIMD)
+// fits on a CU beside two k_gemm_x3h blocks (2 x 66 KB, 2 x 224 VGPRs per SIMD): the prepare stream
+// launches the next batch's rollout in grids of one block per CU.
+template <int KIND, bool X3, int UNR = 2>
+__global__ __launch_bounds__(256, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                      int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
                                                      uint32_t point_base, const float* __restrict__ gx,
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(256) void k_pis_rollout(EqDev e, NetPisDev pn, cons
                                                      int bx0) {
   __shared__ float xsh[NXP_MAX];
   __shared__ float gsts[4 * P * NSG];
-  pis_rollout_block<KIND, X3>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L,
+  pis_rollout_block<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L,
                               stage, td_dt, xsh, gsts, bx0 + blockIdx.x);
 }
 
