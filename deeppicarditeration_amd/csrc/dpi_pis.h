@@ -285,6 +285,7 @@ __global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float*
   __shared__ float cph[2 * C];                           // coeff | phase
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, jj = lane & 15, qq = lane >> 4;
   const int nsm = min(pn.nsm, NSM_MAX);
+  __builtin_amdgcn_s_setprio(2);  // critical path, above a co-resident prepare-stream rollout wave
   auto stage = [&](const uint32_t* src, int off, int Kp) {
     const int ng = C * Kp / 4;
     for (int idx = tid; idx < ng; idx += PT_THREADS) {
@@ -528,6 +529,7 @@ template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L,
                                                         int n, float* __restrict__ fb) {
   __shared__ PisGmmLds gmm;
+  __builtin_amdgcn_s_setprio(2);
   pis_stage_gmm(e, gmm);
   __syncthreads();
   const int i = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
@@ -618,6 +620,8 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   __shared__ float part[4][4][64];  // per-wave 16-path column sums: [wave][q][value]
   __shared__ float vsum[4][2];      // per-wave sums of the value column and its square
   __shared__ PisGmmLds gmm;
+  // the label call's critical path: above a co-resident prepare-stream rollout wave (as the GEMMs)
+  __builtin_amdgcn_s_setprio(2);
   pis_stage_gmm(e, gmm);
   __syncthreads();
   const int tid = threadIdx.x;
