@@ -140,14 +140,14 @@ def cpu_baseline(wl, sample_paths, target_s=6.0):
     with_gradients + estimate_integral_with_gradients vectorised in PyTorch, pinned to the
     reference's outputs by tests/test_cpu_baseline.py), same equation / network / M, in fp32 and
     fp64 on all the CPUs this process may use (GBM: the SDGD branch of get_f, one autograd pass per
-    sampled index as in the reference).  The Malliavin Hessian labels (gbm_hess): the fp64 numpy
-    oracle on one thread (their _double estimators are not restated in torch)."""
+    sampled index as in the reference; the Malliavin Hessian labels: the _double estimators with the
+    full-Hessian get_f, one autograd pass per state dimension)."""
     import deeppicarditeration_amd as dpi
     from oracle import torch_cpu as TC
     eq, net = _make(wl, dpi)
     cores = TC.host_cores()
     model = TC.cpu_model()
-    if wl["eq"] in ("Cha", "OUProcessEquation") or (wl["eq"] == "GBMEquationComplexExact" and not wl.get("hess")):
+    if wl["eq"] in ("Cha", "OUProcessEquation", "GBMEquationComplexExact"):
         from oracle import dpi_oracle as O
         oeq, _ = _oracle_objects(wl, eq, net)
 
@@ -157,13 +157,18 @@ def cpu_baseline(wl, sample_paths, target_s=6.0):
         res = {}
         for dt, name in ((torch.float32, "fp32"), (torch.float64, "fp64")):
             v, pts, secs, th = TC.time_reference_algorithm(eq, net, points, M, dt, target_s=target_s,
-                                                           points_per_call=1 if (wl.get("pis") or wl.get("sdgd"))
-                                                           else 4, threads=cores, v=wl.get("sdgd") or None)
+                                                           points_per_call=1 if (wl.get("pis") or wl.get("sdgd")
+                                                                                 or wl.get("hess")) else 4,
+                                                           threads=cores, v=wl.get("sdgd") or None,
+                                                           hessians=bool(wl.get("hess")))
             res[name] = {"value": v, "points": pts, "seconds": round(secs, 2)}
         return {"value": res["fp32"]["value"], "unit": "path-labels/s", "cores": cores, "kind": "port",
                 "dtype": "fp32", "fp64": res["fp64"]["value"], "cpu": model,
-                "sample": f"oracle/torch_cpu.py: the reference's estimators (data.py:471-527, 899-926; one Gaussian "
-                          f"jump per path, autograd grad u{' and SDGD u_ii' if wl.get('sdgd') else ''}) in PyTorch on "
+                "sample": (f"oracle/torch_cpu.py: the reference's _double Hessian estimators (data.py:823-897, "
+                           f"1153-1201; two half-steps per path, full-Hessian f by autograd) in PyTorch on "
+                           if wl.get("hess") else
+                           f"oracle/torch_cpu.py: the reference's estimators (data.py:471-527, 899-926; one Gaussian "
+                           f"jump per path, autograd grad u{' and SDGD u_ii' if wl.get('sdgd') else ''}) in PyTorch on ") +
                           f"{cores} host threads, {M} paths per point; "
                           f"fp32 {res['fp32']['points']} points in {res['fp32']['seconds']} s, fp64 "
                           f"{res['fp64']['points']} points in {res['fp64']['seconds']} s"}

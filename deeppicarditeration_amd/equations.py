@@ -353,6 +353,9 @@ class GBMEquationComplexExact(SimpleDiffusionEquationWithHessian):
     def hess_diag(self, t, x):
         return -torch.sin(self._arg(t, x)) @ (self.v * self.w[:, 1:] ** 2).to(x)
 
+    def ffh(self, t, x, u, u_x, hess_u):  # equations.py:476-478 (full Hessian: its diagonal)
+        return self.ffi(t, x, u, torch.diagonal(hess_u, dim1=1, dim2=2))
+
     def ffi(self, t, x, u, u_ii):
         lap = self.d * u_ii.mean(-1, keepdim=True)
         nonlin = self.d * u_ii.abs().mean(-1, keepdim=True)

@@ -115,7 +115,80 @@ def labels_reference_algorithm(eq, net, tx, M, gen, noise=None, v=None):
     return y + c.view(n, M, 1 + nx).mean(1)
 
 
-def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, points_per_call=4, threads=None, v=None):
+def _f_full_hessian(eq, net, s, X):
+    """f with the full Hessian of u (get_f without a Hessian approximation, data.py:1259-1272: one
+    autograd pass per state dimension, create_graph as there; ZeroSolution: zero derivatives)."""
+    X = X.detach().requires_grad_(True)
+    nx = X.shape[1]
+    with torch.enable_grad():
+        u = net(torch.cat([s, X], -1))
+        ux = torch.autograd.grad(u.sum(), X, create_graph=True, allow_unused=True)[0] if u.requires_grad else None
+        if ux is None:
+            ux = torch.zeros_like(X)
+            hess = torch.zeros(X.shape[0], nx, nx, dtype=X.dtype)
+        else:
+            hess = torch.zeros(X.shape[0], nx, nx, dtype=X.dtype)
+            for i in range(nx):
+                (h,) = torch.autograd.grad(ux[:, i], X, grad_outputs=torch.ones_like(ux[:, i]), create_graph=True)
+                hess[:, i, :] = h.detach()
+    return eq.ffh(s, X.detach(), u.detach(), ux.detach(), hess)
+
+
+def labels_hessians_reference_algorithm(eq, net, tx, M, gen, noise=None):
+    """(n, 1+nx+nx^2) Malliavin Hessian labels of generate_with_gradients_and_hessians: the terminal
+    (data.py:1153-1201) and integral (:823-897) _double estimators, each with its two half-step
+    rollout, for an equation with a full-Hessian nonlinearity (GBMEquationComplexExact).  `noise` =
+    (terminal dW1, dW2, N1, U, integral dW1, dW2, N2), R = n M rows each (make_golden.py's draw order)."""
+    n, nx = tx.shape[0], eq.nx
+    dt = tx.dtype
+    T = float(eq.T)
+    a = math.sqrt(float(eq.alpha))
+    R = n * M
+    draw = iter(noise) if noise is not None else None
+
+    def rn():
+        return next(draw) if draw is not None else torch.randn(R, nx, generator=gen, dtype=dt)
+
+    t = tx[:, :1].repeat_interleave(M, 0)
+    x = tx[:, 1:].repeat_interleave(M, 0)
+    ones = torch.ones(R, 1, dtype=dt)
+    eye = torch.eye(nx, dtype=dt)
+    # terminal
+    t_mid = (T + t) / 2
+    Xm = x + torch.sqrt(t_mid - t) * a * rn()
+    XT = Xm + torch.sqrt(T - t_mid) * a * rn()
+    Y = (XT - x) / torch.sqrt(T - t) / a / torch.sqrt(T - t)
+    g_single = eq.g(tx[:, 1:])
+    g = g_single.repeat_interleave(M, 0)
+    term = ((eq.g(XT) - g) * torch.cat([ones, Y], -1)).view(n, M, -1).mean(1)
+    term[:, :1] += g_single
+    W1 = torch.sqrt(T - t) * rn()
+    dg = (eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g) / 2 / (T - t)
+    p1 = ((dg / (T - t)).unsqueeze(-1) * torch.einsum("ij,ik->ijk", W1, W1)).view(n, M, -1).mean(1)
+    p2 = dg.view(n, M, 1).mean(1, keepdim=True) * eye.reshape(1, 1, nx * nx)
+    term_h = p1 - p2.view(n, -1)
+    # integral
+    U = next(draw) if draw is not None else torch.rand(R, 1, generator=gen, dtype=dt)
+    s = U * (T - t) + t + 0.0001
+    sm = (s + t) / 2
+    Xm = x + torch.sqrt(sm - t) * a * rn()
+    Xs = Xm + torch.sqrt(s - sm) * a * rn()
+    Ys = (Xs - x) / torch.sqrt(s - t) / a / torch.sqrt(s - t)
+    fb_single = _f_full_hessian(eq, net, tx[:, :1], tx[:, 1:])
+    fb = fb_single.repeat_interleave(M, 0)
+    tt = tx[:, :1]
+    intg = ((T - t) * (_f_full_hessian(eq, net, s, Xs) - fb) * torch.cat([ones, Ys], -1)).view(n, M, -1).mean(1)
+    intg[:, :1] += fb_single * (T - tt)
+    W2 = torch.sqrt(s - t) * rn()
+    df = (_f_full_hessian(eq, net, s, x + a * W2) + _f_full_hessian(eq, net, s, x - a * W2) - 2 * fb) / 2 / (s - t)
+    p1 = ((df / (s - t)).unsqueeze(-1) * torch.einsum("ij,ik->ijk", W2, W2)).view(n, M, -1).mean(1)
+    p2 = df.view(n, M, 1).mean(1, keepdim=True) * eye.reshape(1, 1, nx * nx)
+    intg_h = (p1 - p2.view(n, -1)) * (T - tt)
+    return torch.cat([term + intg, term_h + intg_h], -1)
+
+
+def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, points_per_call=4, threads=None, v=None,
+                             hessians=False):
     """path-labels/s of labels_reference_algorithm on `threads` host threads for ~target_s seconds."""
     threads = threads or host_cores()
     prev = torch.get_num_threads()
@@ -124,12 +197,14 @@ def time_reference_algorithm(eq, net, sample_points, M, dtype, target_s=8.0, poi
     gen = torch.Generator().manual_seed(0)
     done = calls = 0
     try:
-        labels_reference_algorithm(eq, net, sample_points(points_per_call, 0).to(dtype), M, gen, v=v)  # warm-up
+        label = ((lambda tx: labels_hessians_reference_algorithm(eq, net, tx, M, gen)) if hessians
+                 else (lambda tx: labels_reference_algorithm(eq, net, tx, M, gen, v=v)))
+        label(sample_points(points_per_call, 0).to(dtype))  # warm-up
         t0 = time.perf_counter()
         while True:
             tx = sample_points(points_per_call, calls * points_per_call).to(dtype)
             # (no finiteness check: in fp32 the reference's s - t rounds to 0 for tiny U, giving inf)
-            labels_reference_algorithm(eq, net, tx, M, gen, v=v)
+            label(tx)
             done += points_per_call * M
             calls += 1
             dt = time.perf_counter() - t0
