@@ -1107,16 +1107,31 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   }
   float Cb = 0.f;
   if constexpr (KIND == DPI_EQ_GBM) {
-    // exact-solution part of ffi at (t, x) (equations.py:457-466)
+    // exact-solution part of ffi at (t, x) (equations.py:457-466); the NSG dot products w_c . x
+    // reduced together (one barrier pair instead of one per component, each sum in block_sum_b's order)
     float arg[NSG], sn[NSG];
+    {
+      __shared__ float redw[NTHB / 64][NSG];
+      float v[NSG];
 #pragma unroll
-    for (int c = 0; c < NSG; ++c) {
-      float v = 0.f;
-      if (c < e.nodes)
-        for (int d = tid; d < nx; d += NTHB) v = fmaf(e.gw[c * F + 1 + d], xs[d], v);
-      v = block_sum_b(v, red);
-      arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, v) : 0.f;
-      sn[c] = __sinf(arg[c]);
+      for (int c = 0; c < NSG; ++c) {
+        v[c] = 0.f;
+        if (c < e.nodes)
+          for (int d = tid; d < nx; d += NTHB) v[c] = fmaf(e.gw[c * F + 1 + d], xs[d], v[c]);
+        v[c] = wave_sum(v[c]);
+      }
+      __syncthreads();
+      if ((tid & 63) == 0)
+#pragma unroll
+        for (int c = 0; c < NSG; ++c) redw[tid >> 6][c] = v[c];
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float a = 0.f;
+        for (int w = 0; w < NTHB / 64; ++w) a += redw[w][c];
+        arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, a) : 0.f;
+        sn[c] = __sinf(arg[c]);
+      }
     }
     const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
     Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
