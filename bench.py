@@ -4,11 +4,13 @@ One step = one `sample_with_gradients` pass over one synthetic batch: Philox poi
 per-point baseline, the fused K-step rollout + u / grad u + label-moment kernel, (for N > 1) the
 RCCL all-gather of per-rank label moments and their fixed-order reduction, finalize.
 
-Workload (N = 1): BASELINE configs[1] — Burgers (Cha, nx = 100, k = 5, T = 1), 4x128 ELU MLP
-(random init, torch.manual_seed(0)), 16 points x M = 4096 MC paths = 65,536 path-labels,
-K = 50 Euler–Maruyama steps.  For N GPUs (weak scaling, BASELINE configs[3] pattern) each rank
-owns MC indices [r*4096, (r+1)*4096) of the same 16 points (global M = 4096 N), and the label
-moments are combined with one all-gather over RCCL + dpi_moments_reduce.
+Workload (N = 1, default): BASELINE configs[1] — Burgers (Cha, nx = 100, k = 5, T = 1), 4x128 ELU
+MLP (random init, torch.manual_seed(0)), 16 points x M = 4096 MC paths = 65,536 path-labels,
+K = 50 Euler–Maruyama steps.  N > 1 (default): BASELINE configs[3] — Burgers, 512 points x 4096 MC
+paths = 2M path-labels per step in total (strong scaling), rank r owning MC indices
+[r 4096/N, (r+1) 4096/N) of the same 512 points, label moments combined with one all-gather over
+RCCL + dpi_moments_reduce (`--workload burgers_cfg3` runs the same at N = 1; `--workload burgers`
+at N > 1 is the weak-scaling variant, 4096 paths per GPU).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
@@ -42,6 +44,12 @@ WORKLOADS = {
     "burgers": dict(cfg="configs[1]", eq="Cha", widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0,
                     flop=2.72e5, peak="split", kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
                                       "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)"),
+    "burgers_cfg3": dict(cfg="configs[3]", eq="Cha", widths=[128] * 4, points=512, m_total=4096, K=50, sdgd=0,
+                         flop=2.72e5, peak="split", scaling="strong",
+                         kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call",
+                         desc="Burgers 100d T=1 (Cha k=5), 512 points x 4096 MC paths = 2,097,152 path-labels per step "
+                              "in total, MC-sharded 4096/N paths per GPU, K=50 EM steps, MLP 101-128x4-1 ELU, one RCCL "
+                              "all-gather of label moments + canonical tree reduce (BASELINE configs[3])"),
     "hjb": dict(cfg="configs[2]", eq="OUProcessEquation", widths=[512] * 4, pis=True, points=64, m_per_gpu=4096, K=50,
                 sdgd=0, flop=3.73e6, peak="split", kernel="k_pis_rollout + k_gemm_x3 chain (fp16-split) + "
                                                            "k_pis_final + k_reduce per dpi_label_moments call",
@@ -69,7 +77,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed steps for this long before the warmup")
     ap.add_argument("--cpu-sample-paths", type=int, default=512, help="MC paths per point in the CPU sample")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="burgers")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: burgers (configs[1]) at N = 1, burgers_cfg3 (configs[3], 2M paths MC-sharded "
+                         "over the N GPUs) at N > 1")
     ap.add_argument("--pipelined", action="store_true", help="two-phase labels also at N = 1 (default: N > 1 only)")
     ap.add_argument("--prepare", action="store_true", help="two-phase labels with the next batch's sampling and "
                                                            "baseline on a low-priority side stream, the path "
@@ -153,7 +163,7 @@ def cpu_baseline(wl, sample_paths, target_s=6.0):
 
         def points(n, base):
             return torch.from_numpy(O.sample_points(oeq, n, seed=1, point_base=base))
-        M = wl["m_per_gpu"]
+        M = wl.get("m_per_gpu", wl.get("m_total"))
         res = {}
         for dt, name in ((torch.float32, "fp32"), (torch.float64, "fp64")):
             v, pts, secs, th = TC.time_reference_algorithm(eq, net, points, M, dt, target_s=target_s,
@@ -208,6 +218,8 @@ def main():
     # PISGradNet workloads: the next batch's sampling and baseline run on a low-priority side stream
     # while this batch's GEMM chain runs on a high-priority one (HJB 6.19 -> 5.92 ms/step).  Not for
     # the fused-kernel workloads, whose one path launch the side work would slow.
+    if args.workload is None:
+        args.workload = "burgers" if world == 1 else "burgers_cfg3"
     args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis"))) and not args.no_prepare
     if args.prepare:
         lo, hi = torch.cuda.Stream.priority_range()
@@ -222,10 +234,17 @@ def main():
     from deeppicarditeration_amd.sharding import ShardedLabeler
 
     wl = WORKLOADS[args.workload]
-    N_POINTS, M_PER_GPU, K_STEPS = wl["points"], wl["m_per_gpu"], wl["K"]
+    N_POINTS, K_STEPS = wl["points"], wl["K"]
+    if "m_total" in wl:  # strong scaling: the configs[3] total MC width split over the ranks
+        M = wl["m_total"]
+        if M % (64 * world):
+            raise SystemExit(f"{args.workload}: M = {M} is not a multiple of 64 x {world} ranks")
+        M_PER_GPU = M // world
+    else:  # weak scaling: every rank owns m_per_gpu MC indices of the same points
+        M_PER_GPU = wl["m_per_gpu"]
+        M = M_PER_GPU * world
     FLOP_PER_PATH_LABEL = wl["flop"]
     eq, net = _make(wl, dpi)
-    M = M_PER_GPU * world
     hess = {"method": "SDGD", "kwargs": {"v": wl["sdgd"]}} if wl["sdgd"] else None
     gen = dpi.OnlineDataGenerator(eq, net, 80, 1, device=dev, t_always_uniform=True, n_estimate_terminal=M,
                                   n_estimate_integral=M, n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
@@ -338,7 +357,7 @@ def main():
     # u = 0 (ZeroSolution: same Philox streams, same K-step EM, no network), i.e. the
     # Philox4x32-10 + Box-Muller VALU issue the noise contract fixes.
     floor_ms = None
-    if rank == 0 and not wl.get("pis") and not wl.get("hess"):
+    if rank == 0 and not wl.get("pis") and not wl.get("hess") and "m_total" not in wl:
         gen0 = dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(1), 80, 1, device=dev, t_always_uniform=True,
                                        n_estimate_terminal=M_PER_GPU, n_estimate_integral=M_PER_GPU,
                                        n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
@@ -373,7 +392,10 @@ def main():
         # (profiles/valu_<workload>.json; the kernel's instruction stream is fixed, so they are a constant
         # of the launch); the launch time is measured live.
         valu = None
-        vf = ROOT / "profiles" / f"valu_{args.workload}.json"
+        # per-launch PMC figures are measured per workload and rank count (a configs[3] rank's launch
+        # at N GPUs is 512 points x 4096/N paths): profiles/<kind>_<workload>[_n<N>].json
+        prof_tag = args.workload + (f"_n{world}" if "m_total" in wl and world > 1 else "")
+        vf = ROOT / "profiles" / f"valu_{prof_tag}.json"
         if vf.exists() and not wl.get("pis"):
             kern = json.loads(vf.read_text())["kernels"]
             # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD>: the network launch, not the u = 0 twin
@@ -381,13 +403,22 @@ def main():
             busy = max(net_k, key=lambda v: v["dispatches"])["valu_busy_cycles_per_simd"]
             valu = {"achieved": busy * N_SIMD / (k_ms * 1e-3) / 1e12, "peak": N_SIMD * PEAK_CLOCK_GHZ * 1e9 / 1e12,
                     "unit": "T VALU-busy SIMD-cycles/s", "valu_busy_cycles_per_simd": busy,
-                    "busy_source": f"profile_derived: profiles/valu_{args.workload}.json (SQ_ACTIVE_INST_VALU x 4 / "
+                    "busy_source": f"profile_derived: profiles/valu_{prof_tag}.json (SQ_ACTIVE_INST_VALU x 4 / "
                                    "1024 SIMDs per launch)"}
             valu["frac"] = valu["achieved"] / valu["peak"]
         traffic = None
-        tf = ROOT / "profiles" / f"traffic_{args.workload}.json"
+        tf = ROOT / "profiles" / f"traffic_{prof_tag}.json"
         if tf.exists():
             traffic = json.loads(tf.read_text()).get("hbm_bytes_per_launch")
+        ms_step = dt / args.steps * 1e3
+        hbm = None
+        if traffic is not None:
+            # HBM bytes of one label call (PMC) against the 8 TB/s peak, over the live step time and over
+            # the live launch time of the measured launches
+            hbm = {"bytes_per_call": traffic, "GB_per_s": traffic / (ms_step * 1e-3) / 1e9,
+                   "GB_per_s_kernel": traffic / (k_ms * 1e-3) / 1e9, "peak_GB_per_s": PEAK_HBM_GBS}
+            hbm["frac_of_8TBs"] = hbm["GB_per_s"] / PEAK_HBM_GBS
+            hbm["frac_of_8TBs_kernel"] = hbm["GB_per_s_kernel"] / PEAK_HBM_GBS
         out = {
             "metric": "SDE-path labels/sec (100-d, 50 Euler steps) per GPU; rel-L2 vs ref",
             "value": value,
@@ -395,9 +426,9 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": dt / args.steps * 1e3,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl.get("scaling", "weak"),
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (Philox-sampled collocation points; random-init ELU MLP, torch.manual_seed(0))",
@@ -415,6 +446,7 @@ def main():
                          "traffic_source": (f"profile_derived: profiles/traffic_{args.workload}.json (rocprofv3 PMC "
                                             "FETCH_SIZE / WRITE_SIZE passes of this bench command, HBM bytes per "
                                             "label call)") if traffic is not None else None,
+                         "hbm": hbm,
                          "kernel": wl["kernel"], "kernel_ms": k_ms,
                          "valu": valu, "mfma": mfma},
         }
@@ -426,7 +458,7 @@ def main():
                         "VALU-issue floor of the noise contract (2 x K x nx normals per path-label)",
                 "kernel_ms": floor_ms, "frac": floor_ms / k_ms}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_paths if args.workload == "burgers" else 64)
+            out["cpu_baseline"] = cpu_baseline(wl, args.cpu_sample_paths if wl["eq"] == "Cha" else 64)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -44,8 +44,17 @@ def build(force=False, verbose=True):
         subprocess.run(cmd, check=True)
         return obj
 
-    with ThreadPoolExecutor(max_workers=len(UNITS)) as ex:
-        objs = list(ex.map(compile_unit, UNITS))
+    headers = sorted(CSRC.glob("*.h")) + [REPO / "include" / "dpi.h"]
+    newest_header = max(h.stat().st_mtime for h in headers)
+
+    def stale(u):  # an object is rebuilt when its unit or any shared header is newer
+        obj = OBJ / (Path(u).stem + ".o")
+        return force or not obj.exists() or obj.stat().st_mtime < max(newest_header, (CSRC / u).stat().st_mtime)
+
+    todo = [u for u in UNITS if stale(u)]
+    with ThreadPoolExecutor(max_workers=max(1, len(todo))) as ex:
+        list(ex.map(compile_unit, todo))
+    objs = [OBJ / (Path(u).stem + ".o") for u in UNITS]
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -10,7 +10,9 @@
 #include <cstdlib>
 #include <type_traits>
 #include <algorithm>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dpi.h"
@@ -1232,6 +1234,31 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   return 0;
 }
 
+// The DPI_PREPARED contract: a prepared label-moments call trusts that dpi_label_prepare staged
+// the first chunk in the same workspace with the same arguments.  dpi_label_prepare records the
+// arguments per workspace (host side: no device read, no sync); the prepared call must match them
+// and consumes the record, so a mismatched or repeated call fails with DPI_ERR_ARG instead of
+// producing labels from another batch's rollout.
+struct PrepTag {
+  const void *p, *net, *tx;
+  int n, M, K, m_begin, m_end, flags;
+  uint64_t seed;
+  uint32_t epoch, point_base;
+  size_t ws_bytes;
+  bool operator==(const PrepTag& o) const {
+    return p == o.p && net == o.net && tx == o.tx && n == o.n && M == o.M && K == o.K && m_begin == o.m_begin &&
+           m_end == o.m_end && flags == o.flags && seed == o.seed && epoch == o.epoch && point_base == o.point_base &&
+           ws_bytes == o.ws_bytes;
+  }
+};
+static std::mutex g_prep_mu;
+static std::unordered_map<const void*, PrepTag>& prep_tags() {
+  static std::unordered_map<const void*, PrepTag> m;
+  return m;
+}
+
+static bool stages_prepare(dpi_problem p, dpi_net net) { return net->d.kind == 2 && !(p->td_dt > 0.f); }
+
 int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,
                       uint32_t point_base, int m_begin, int m_end, int flags, void* ws, size_t ws_bytes, void* stream) {
   WsLayout w;
@@ -1239,13 +1266,36 @@ int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   int rc = label_args(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags & DPI_BOTH, false, nullptr,
                       ws, ws_bytes, &w, &a);
   if (rc || n == 0) return rc;
-  if (net->d.kind != 2 || p->td_dt > 0.f) return 0;  // nothing to stage: the fused path kernels do it all
+  if (!stages_prepare(p, net)) return 0;  // nothing to stage: the fused path kernels do it all
+  {
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    prep_tags()[ws] = PrepTag{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, seed, epoch, point_base, ws_bytes};
+  }
   return pis_paths(p, net, tx, n, K, a, w, (char*)ws, (hipStream_t)stream, false, true);
+}
+
+static int check_prepared(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
+                          uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, void* ws,
+                          size_t ws_bytes) {
+  if (!(flags & DPI_PREPARED) || n == 0 || !p || !net || !stages_prepare(p, net)) return 0;
+  const PrepTag want{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, seed, epoch, point_base, ws_bytes};
+  std::lock_guard<std::mutex> g(g_prep_mu);
+  auto it = prep_tags().find(ws);
+  if (it == prep_tags().end())
+    return fail(DPI_ERR_ARG, "label_moments: DPI_PREPARED without a dpi_label_prepare on this workspace");
+  const bool same = it->second == want;
+  prep_tags().erase(it);
+  if (!same)
+    return fail(DPI_ERR_ARG, "label_moments: DPI_PREPARED arguments differ from the dpi_label_prepare call on this "
+                             "workspace (points, counters, MC range, flags or workspace size)");
+  return 0;
 }
 
 int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,
                       uint32_t point_base, int m_begin, int m_end, int flags, float* moments, void* ws,
                       size_t ws_bytes, void* stream) {
+  int rc = check_prepared(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, ws, ws_bytes);
+  if (rc) return rc;
   return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, moments, ws, ws_bytes,
                       stream, nullptr, 0.f);
 }
@@ -1254,6 +1304,8 @@ int dpi_label_moments_finalize(dpi_problem p, dpi_net net, const float* tx, int 
                                uint32_t epoch, uint32_t point_base, int flags, float sample_bound, float* y,
                                float* moments, void* ws, size_t ws_bytes, void* stream) {
   if (n > 0 && !y) return fail(DPI_ERR_ARG, "label_moments_finalize: null y");
+  int rc = check_prepared(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, ws, ws_bytes);
+  if (rc) return rc;
   return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, moments, ws, ws_bytes, stream, y,
                       sample_bound);
 }

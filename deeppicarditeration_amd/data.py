@@ -61,7 +61,7 @@ class OnlineDataGenerator:
                  device: Union[str, torch.device] = "cuda", t_always_uniform=False, n_estimate_terminal=1,
                  n_estimate_integral=1, hessian_approximation=None, sample_bound=None, estimate_terminal="OU_ByGx",
                  estimate_integral="OU_Simple", estimate_delta_t=0.0, n_euler_steps: int = 50, seed: int = 0,
-                 epoch: int = None):
+                 epoch: int = None, max_points_per_call: int = None, label_dtype: torch.dtype = torch.float32):
         if not (isinstance(equation, SimpleDiffusionEquation) or isinstance(equation, OUProcessEquation)):
             raise AssertionError("Currently only SimpleDiffusionEquation and OUProcessEquation are supported")  # :426-429
         if equation.nu != 1:
@@ -111,6 +111,17 @@ class OnlineDataGenerator:
         self.sdgd_v = sdgd_v
         self._configure_problem()
         self._ws = None
+        # Points per generator call of the dataset surface (None: unbounded).  The reference sizes
+        # its calls by probing GPU memory (picard/memory.py:95-171): a dataset whose calls exceed
+        # this cap raises torch.cuda.OutOfMemoryError, which those probes read as "does not fit",
+        # so NEW_SAMPLING settles at the cap instead of at a size only HBM capacity bounds.
+        self.max_points_per_call = None if max_points_per_call is None else int(max_points_per_call)
+        # dtype of the (tx, labels) the sample_* surface returns: labels are computed in fp32; a
+        # data module running DATA.FLOAT: double (picard/config.py:194-200 sets the default dtype, so
+        # its networks are fp64) receives them cast exactly to fp64
+        if label_dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"label_dtype must be float32 or float64 (got {label_dtype})")
+        self.label_dtype = label_dtype
 
     def _configure_problem(self):
         """The device problem handle belongs to the equation and may be shared by several
@@ -158,15 +169,20 @@ class OnlineDataGenerator:
                                                 self.t_factors, _ptr(tx), _stream(self._device)), "dpi_sample_points_t")
         return tx, pb
 
+    def _out(self, tx, y):
+        if self.label_dtype == torch.float32:
+            return tx, y
+        return tx.to(self.label_dtype), y.to(self.label_dtype)
+
     def sample_with_gradients(self, n_batch):
         """data.py:211-223: (tx, clip(u_ux)) with u_ux (n, 1+nx)."""
         tx, pb = self.sample_t_and_x(n_batch)
-        return tx, self._generate(tx, pb, _lib.DPI_BOTH)
+        return self._out(tx, self._generate(tx, pb, _lib.DPI_BOTH))
 
     def sample_with_gradients_and_hessians(self, n_batch):
         """data.py:225-237: (tx, clip(u_ux_uxx)) with u_ux_uxx (n, 1 + nx + nx^2)."""
         tx, pb = self.sample_t_and_x(n_batch)
-        return tx, self._generate_hess(tx, pb, self.sample_bound)
+        return self._out(tx, self._generate_hess(tx, pb, self.sample_bound))
 
     def generate_with_gradients_and_hessians(self, tx, point_base=None):
         """data.py:1220-1223: Malliavin-weight Hessian labels (no clip), (n, 1 + nx + nx^2)."""
@@ -201,7 +217,7 @@ class OnlineDataGenerator:
         """data.py:196-209: (tx, clip(u)) with u (n, 1)."""
         tx, pb = self.sample_t_and_x(n_batch)
         u = self.generate(tx, pb)
-        return tx, torch.clamp(u, -self.sample_bound, self.sample_bound)
+        return self._out(tx, torch.clamp(u, -self.sample_bound, self.sample_bound))
 
     # ------------------------------------------------------------------ exact labels (closed form)
     def _t_x(self, n_batch):
@@ -212,14 +228,14 @@ class OnlineDataGenerator:
         """data.py:239-250: (tx, u*(t, x))."""
         tx, t, x = self._t_x(n_batch)
         with torch.no_grad():
-            return tx, self.equation.exact_solution(t, x).to(tx)
+            return self._out(tx, self.equation.exact_solution(t, x).to(tx))
 
     def sample_exact_with_gradients(self, n_batch):
         """data.py:252-263: (tx, [u*, grad u*])."""
         tx, t, x = self._t_x(n_batch)
         with torch.no_grad():
             u, ux = self.equation.u_u_x(t, x)
-        return tx, torch.cat([u.to(tx), ux.to(tx)], -1)
+        return self._out(tx, torch.cat([u.to(tx), ux.to(tx)], -1))
 
     def sample_exact_with_gradients_and_hessians(self, n_batch):
         """data.py:265-283: (tx, [u*, grad u*, Hess u*]) — equations with a Hessian term only."""
@@ -228,29 +244,36 @@ class OnlineDataGenerator:
         tx, t, x = self._t_x(n_batch)
         with torch.no_grad():
             u, ux, uh = self.equation.u_u_x_u_hessian(t, x)
-        return tx, torch.cat([u.to(tx), ux.to(tx), uh.reshape(u.shape[0], -1).to(tx)], -1)
+        return self._out(tx, torch.cat([u.to(tx), ux.to(tx), uh.reshape(u.shape[0], -1).to(tx)], -1))
 
     # ------------------------------------------------------------------ datasets (data.py:285-335)
+    def _dataset(self, n_total, n_batch_buffer, batch_size, sampler):
+        ds = IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, sampler)
+        cap = self.max_points_per_call
+        if cap is not None and ds._n_samples_each_call > cap:
+            raise torch.cuda.OutOfMemoryError(
+                f"{ds._n_samples_each_call} points per generator call (n_batch_buffer {n_batch_buffer} x batch_size "
+                f"{batch_size}) exceed the generator's max_points_per_call = {cap} (DATA.POINTS_PER_CALL)")
+        return ds
+
     def dataset(self, n_total, n_batch_buffer, batch_size):
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample)
 
     def dataset_with_gradients(self, n_total, n_batch_buffer, batch_size):
         """The boundary: the buffered iterable dataset over sample_with_gradients."""
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_with_gradients)
 
     def dataset_with_gradients_and_hessians(self, n_total, n_batch_buffer, batch_size):
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size,
-                                                self.sample_with_gradients_and_hessians)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_with_gradients_and_hessians)
 
     def dataset_exact(self, n_total, n_batch_buffer, batch_size):
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_exact)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact)
 
     def dataset_exact_with_gradients(self, n_total, n_batch_buffer, batch_size):
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients)
 
     def dataset_exact_with_gradients_and_hessians(self, n_total, n_batch_buffer, batch_size):
-        return IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size,
-                                                self.sample_exact_with_gradients_and_hessians)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients_and_hessians)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
     def workspace_bytes(self, n, M, hessians=False):

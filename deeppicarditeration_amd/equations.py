@@ -198,19 +198,29 @@ class ComplexDiffusionEquation(DiffusionEquation):
     has_hessian_term = False
 
     def __init__(self, nx, T, theta: float = 1.0, mu: float = 0.0, alpha: float = 1.0, num_components=2,
-                 mean_scale=1.0, var_scale=2.0, alpha_scale=4.0, **kwargs):
+                 mean_scale=1.0, var_scale=2.0, alpha_scale=4.0, mean=None, var=None, pi=None, **kwargs):
+        """mean (K, nx), var (K, nx) diagonals, pi (K): the mixture's parameters when given (the
+        reference-side binding passes the reference equation's own tensors); otherwise loaded as the
+        reference loads them (equations.py:525-544)."""
         super().__init__(nx=nx, T=T, alpha=alpha, **kwargs)
         self.theta = float(theta)
         self.mu = float(mu)
         self.d = float(nx)
         self.num_components = num_components
         tag = f"{nx}d_ms={mean_scale}_vs={var_scale}_{num_components}"
-        self.mean = _load_param(f"mean_{tag}.pt", f"mean_{tag}.npy")
-        self.pi = _load_param(f"pi_{tag}.pt", f"pi_{tag}.npy")
-        try:
-            self.var = torch.diagonal(_load_param(f"var_{tag}.pt", f"var_{tag}.npy"), dim1=-2, dim2=-1)
-        except FileNotFoundError:  # SURVEY.md finding 8: var = var_scale * I (equations.py:539)
-            self.var = var_scale * torch.ones(num_components, nx, dtype=torch.float64)
+        f64 = lambda a: torch.as_tensor(a).detach().cpu().to(torch.float64)  # noqa: E731
+        self.mean = f64(mean) if mean is not None else _load_param(f"mean_{tag}.pt", f"mean_{tag}.npy")
+        self.pi = f64(pi) if pi is not None else _load_param(f"pi_{tag}.pt", f"pi_{tag}.npy")
+        if var is not None:
+            self.var = f64(var)
+        else:
+            try:
+                self.var = torch.diagonal(_load_param(f"var_{tag}.pt", f"var_{tag}.npy"), dim1=-2, dim2=-1)
+            except FileNotFoundError:  # SURVEY.md finding 8: var = var_scale * I (equations.py:539)
+                self.var = var_scale * torch.ones(num_components, nx, dtype=torch.float64)
+        if self.mean.shape != (num_components, nx) or self.var.shape != (num_components, nx) or \
+                self.pi.shape != (num_components,):
+            raise ValueError("GMM parameters: mean and var (num_components, nx), pi (num_components,)")
         self.gmm_calc = GaussianMixtureDiagonalCovariance(self.mean, self.var, self.pi)
         self.alpha_scale = float(alpha_scale)
         self.alpha_init = alpha_scale * float(alpha)
@@ -309,11 +319,14 @@ class GBMEquationComplexExact(SimpleDiffusionEquationWithHessian):
 
     supported_approximate_methods = ("SDGD",)
 
-    def __init__(self, nx: int, alpha: float = 1.0, T: float = 1.0, case: str = "case_1"):
+    def __init__(self, nx: int, alpha: float = 1.0, T: float = 1.0, case: str = "case_1", w=None, v=None):
+        """w (nodes, 1 + nx), v (nodes, 1): given (the reference-side binding passes the reference
+        equation's tensors), or loaded as the reference loads them (equations.py:408-419)."""
         super().__init__(nx=nx, alpha=alpha, T=T)
         self.d = float(nx)
-        self.w = _load_param(f"gbm_2nodes_w_{nx}d.pt", f"gbm_2nodes_w_{nx}d_{case}.npy")
-        self.v = _load_param(f"gbm_2nodes_v_{nx}d.pt", f"gbm_2nodes_v_{nx}d_{case}.npy")
+        f64 = lambda a: torch.as_tensor(a).detach().cpu().to(torch.float64)  # noqa: E731
+        self.w = f64(w) if w is not None else _load_param(f"gbm_2nodes_w_{nx}d.pt", f"gbm_2nodes_w_{nx}d_{case}.npy")
+        self.v = f64(v) if v is not None else _load_param(f"gbm_2nodes_v_{nx}d.pt", f"gbm_2nodes_v_{nx}d_{case}.npy")
 
     def _arg(self, t, x):
         t = torch.as_tensor(t, dtype=x.dtype, device=x.device) * torch.ones(x.shape[0], 1, dtype=x.dtype,
@@ -374,3 +387,32 @@ class GBMEquationComplexExact(SimpleDiffusionEquationWithHessian):
                                               w.ctypes.data_as(dp), v.ctypes.data_as(dp), h),
                    "dpi_problem_create_gbm")
         return h
+
+
+def from_reference(eq) -> Equation:
+    """The device-backed equation for a reference `picard.equations` object (the reference-side
+    binding receives the data module's own equation, picard/data.py:1474-1481): same class name,
+    parameters read from the object — Cha (nx, alpha, k = k' sqrt(nx), T; equations.py:283-290),
+    OUProcessEquation (nx, T, theta, mu, alpha, alpha_scale = alpha_init / alpha, the GMM's mean /
+    var / pi tensors; equations.py:503-558, 609-619), GBMEquationComplexExact (nx, alpha, T, w, v;
+    equations.py:403-419).  An equation of this package is returned as is; any other class raises."""
+    if isinstance(eq, Equation):
+        return eq
+    name = type(eq).__name__
+    f = lambda a: float(torch.as_tensor(a))  # noqa: E731
+    if name == "Cha":
+        return Cha(nx=int(eq.nx), alpha=f(eq.alpha), k=f(eq.k) * math.sqrt(int(eq.nx)), T=f(eq.T))
+    if name == "OUProcessEquation":
+        var = torch.as_tensor(eq.var).detach().cpu().to(torch.float64)
+        if var.dim() == 3:  # (K, nx, nx) covariance matrices (equations.py:539): diagonal mixtures only
+            diag = torch.diagonal(var, dim1=-2, dim2=-1)
+            if not torch.equal(var, torch.diag_embed(diag)):
+                raise NotImplementedError("OUProcessEquation with non-diagonal GMM covariances")
+            var = diag
+        return OUProcessEquation(nx=int(eq.nx), T=f(eq.T), theta=f(eq.theta), mu=f(eq.mu), alpha=f(eq.alpha),
+                                 num_components=int(eq.num_components), alpha_scale=f(eq.alpha_init) / f(eq.alpha),
+                                 mean=eq.mean, var=var, pi=eq.pi)
+    if name == "GBMEquationComplexExact":
+        return GBMEquationComplexExact(nx=int(eq.nx), alpha=f(eq.alpha), T=f(eq.T), w=eq.w, v=eq.v)
+    raise NotImplementedError(f"{name}: no device plugin in this build (Cha, OUProcessEquation, "
+                              "GBMEquationComplexExact)")

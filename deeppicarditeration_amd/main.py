@@ -26,11 +26,18 @@ def train(argv):
         return
     # torchrun --nproc-per-node G -m deeppicarditeration_amd.main train cfg.yaml: one process per GPU,
     # RCCL ("nccl" on ROCm) for the label moments' all-gather and the weight broadcast
+    import datetime
+
     import torch
     import torch.distributed as dist
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # Only rank 0 fits, checkpoints and evaluates; the other ranks wait in the weight broadcast for
+    # that whole time, which at the shipped sizes can exceed the 10-minute default collective
+    # timeout, after which the RCCL watchdog would abort them.  DPI_DIST_TIMEOUT_S (default 6 h)
+    # bounds a wait instead.
+    timeout = datetime.timedelta(seconds=float(os.environ.get("DPI_DIST_TIMEOUT_S", 6 * 3600)))
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     try:
         PicardRunner(cfg, device=f"cuda:{local}", rank=dist.get_rank(), world=dist.get_world_size()).run()
     finally:

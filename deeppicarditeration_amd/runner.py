@@ -84,13 +84,18 @@ class PicardRunner:
         self.device = torch.device(device)
         self.rank, self.world, self.group = int(rank), int(world), group
         self.exp_dir = pathlib.Path(cfg.NAME)
+        err = None
         if self.rank == 0:
-            if self.exp_dir.exists() and any(self.exp_dir.iterdir()):
-                if not cfg.FORCE:
-                    raise FileExistsError(f"Experiment directory {self.exp_dir} already exists.")
-                shutil.rmtree(self.exp_dir)
-            self.exp_dir.mkdir(parents=True, exist_ok=True)
-            (self.exp_dir / "config.yaml").write_text(cfg.dump())
+            try:
+                if self.exp_dir.exists() and any(self.exp_dir.iterdir()):
+                    if not cfg.FORCE:
+                        raise FileExistsError(f"Experiment directory {self.exp_dir} already exists.")
+                    shutil.rmtree(self.exp_dir)
+                self.exp_dir.mkdir(parents=True, exist_ok=True)
+                (self.exp_dir / "config.yaml").write_text(cfg.dump())
+            except Exception as e:  # noqa: BLE001 — re-raised below, after every rank knows
+                err = e
+        self._agree(err, "experiment directory setup")
         if str(cfg.DATA.FLOAT).lower() in ("double", "float64"):  # picard/config.py:194-200
             warnings.warn("DATA.FLOAT: double — the device label path computes in fp32 (labels within the "
                           "north star's rel-L2 <= 1e-4 of the fp64 reference, DESIGN.md); the fit and the "
@@ -108,6 +113,21 @@ class PicardRunner:
         self.i = 0
         self.u_current = ZeroSolution(1)
         self.history = []
+
+    def _agree(self, err, what):
+        """Multi-rank jobs: every rank learns whether any rank failed `what` before the next
+        collective, so a failure on rank 0 alone (existing experiment directory, an exception in the
+        fit) ends every rank with an error instead of leaving the others blocked in the label
+        all-gather or the weight broadcast until the process-group timeout."""
+        if self.world > 1:
+            import torch.distributed as dist
+            dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.device
+            flag = torch.tensor([0.0 if err is None else 1.0], device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            if err is None and float(flag) > 0:
+                raise RuntimeError(f"{what} failed on another rank; stopping this rank")
+        if err is not None:
+            raise err
 
     # ------------------------------------------------------------------ networks
     def new_network(self):
@@ -160,10 +180,17 @@ class PicardRunner:
         opt, sched = make_optimizer(net.parameters(), t.OPTIMIZER)
         n = tx.shape[0]
         bs = int(t.BATCH_SIZE) if t.BATCH_SIZE else n
+        # When the training batch differs from the generation batch (points per generator call), the
+        # reference re-batches through CacheToMemoryWrapper(batch_size, drop_last=True,
+        # shuffle=SHUFFLE) and preloads it (picard/data.py:1718-1731), so even the first epoch comes
+        # from the cache: shuffled under DATA.SHUFFLE and without the partial last batch.  Otherwise
+        # the first epoch streams in draw order and later epochs replay the cache (data.py:1746-1760).
+        rebatched = bs != min(int(self.cfg.DATA.POINTS_PER_CALL), n)
+        shuffle = bool(self.cfg.DATA.SHUFFLE)
         losses = []
         for epoch in range(int(t.N_EPOCHS)):
-            batches = TensorDatasetBuiltInShuffle(tx, y, batch_size=bs,
-                                                  shuffle=bool(self.cfg.DATA.SHUFFLE) and epoch > 0)
+            batches = TensorDatasetBuiltInShuffle(tx, y, batch_size=bs, drop_last=rebatched,
+                                                  shuffle=shuffle and (epoch > 0 or rebatched))
             losses.append(train_steps(net, objective, opt, batches, sched))
         losses = torch.cat(losses) if losses else torch.empty(0)
         return float(losses[-1]) if losses.numel() else float("nan")
@@ -231,31 +258,40 @@ class PicardRunner:
         t_labels = time.perf_counter() - t0
         net = self.new_network()
         rec = None
+        err = None
         if self.rank == 0:
-            if self.cfg.DATA.SAVE:  # data_iter_{i}/split_00.h5 (picard/data.py:1510-1525, data_saver.py:24-56)
-                self.save_labels(tx, y)
-            if self.cfg.NETWORK.RELOAD and self.i > 1:  # picard_iteration.py:249-251
-                net.load_state_dict(torch.load(self.checkpoint_path(self.i - 1), weights_only=True))
-            t1 = time.perf_counter()
-            loss = self.fit(net, tx, y)
-            t_fit = time.perf_counter() - t1
-            torch.save(net.state_dict(), self.checkpoint_path(self.i))
-            metrics = self.evaluate(net)
-            M = int(dict(self.cfg.DATA.kwargs).get("n_estimate_integral", 1))
-            n = int(tx.shape[0])
-            rec = {"iter": self.i, "labels": n, "label_s": t_labels, "labels_per_s": n / t_labels,
-                   "path_labels_per_s": None if self.cfg.DATA.EXACT else n * M / t_labels, "ranks": self.world,
-                   "fit_s": t_fit, "fit": self.fit_kind, "loss": loss, "rel_l2_u": metrics.get("rRMSE"), **metrics}
-            self.history.append(rec)
-            with open(self.exp_dir / "history.jsonl", "a") as f:
-                f.write(json.dumps(rec) + "\n")
-            print(json.dumps(rec), flush=True)
+            try:
+                rec = self._fit_and_record(net, tx, y, t_labels)
+            except Exception as e:  # noqa: BLE001 — re-raised by _agree on this rank
+                err = e
+        self._agree(err, f"Picard iteration {self.i} (fit / checkpoint / evaluation on rank 0)")
         if self.world > 1:  # every rank continues from rank 0's fit
             import torch.distributed as dist
             for v in net.state_dict().values():
                 dist.broadcast(v, src=0, group=self.group)
         self.u_current = net  # frozen by the next OnlineDataGenerator (data.py:409-412)
         return True
+
+    def _fit_and_record(self, net, tx, y, t_labels):
+        if self.cfg.DATA.SAVE:  # data_iter_{i}/split_00.h5 (picard/data.py:1510-1525, data_saver.py:24-56)
+            self.save_labels(tx, y)
+        if self.cfg.NETWORK.RELOAD and self.i > 1:  # picard_iteration.py:249-251
+            net.load_state_dict(torch.load(self.checkpoint_path(self.i - 1), weights_only=True))
+        t1 = time.perf_counter()
+        loss = self.fit(net, tx, y)
+        t_fit = time.perf_counter() - t1
+        torch.save(net.state_dict(), self.checkpoint_path(self.i))
+        metrics = self.evaluate(net)
+        M = int(dict(self.cfg.DATA.kwargs).get("n_estimate_integral", 1))
+        n = int(tx.shape[0])
+        rec = {"iter": self.i, "labels": n, "label_s": t_labels, "labels_per_s": n / t_labels,
+               "path_labels_per_s": None if self.cfg.DATA.EXACT else n * M / t_labels, "ranks": self.world,
+               "fit_s": t_fit, "fit": self.fit_kind, "loss": loss, "rel_l2_u": metrics.get("rRMSE"), **metrics}
+        self.history.append(rec)
+        with open(self.exp_dir / "history.jsonl", "a") as f:
+            f.write(json.dumps(rec) + "\n")
+        print(json.dumps(rec), flush=True)
+        return rec
 
     def run(self):
         for _ in range(self.N):

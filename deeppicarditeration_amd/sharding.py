@@ -10,7 +10,18 @@ per-rank label moments (n, 2, 1+nx) fp32 — 2 x 16 x 101 x 4 B = 12.9 kB per ra
 kernel uses over 64-path blocks.  With M/(64 G) a power of two the labels are bit-identical for
 G = 1, 2, 4, 8.  (The reference has no collective: SURVEY.md §2 rows 18-19.)
 """
+import warnings
+
 import torch
+
+
+_WARNED = set()
+
+
+class ShardBitIdentityWarning(UserWarning):
+    """M / (64 G) is not a power of two: the labels are correct Monte-Carlo means, but the rank
+    sums no longer split the single-call block tree at a power-of-two boundary, so they can differ
+    from the one-GPU labels in the last bits."""
 
 
 class ShardedLabeler:
@@ -25,6 +36,14 @@ class ShardedLabeler:
         if M % (blk * self.world):
             raise ValueError(f"M={M} must be a multiple of 64 x world ({self.world})")
         per = M // self.world
+        nb = per // blk
+        if self.world > 1 and nb & (nb - 1):
+            key = (M, self.world)
+            if key not in _WARNED:
+                _WARNED.add(key)
+                warnings.warn(f"M={M} over {self.world} ranks gives {nb} 64-path blocks per rank, not a power of two: "
+                              "labels will not be bit-identical to the single-GPU labels (the canonical tree splits "
+                              "only at power-of-two block counts)", ShardBitIdentityWarning, stacklevel=2)
         return self.rank * per, (self.rank + 1) * per
 
     def gather_moments(self, mom):

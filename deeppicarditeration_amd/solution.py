@@ -104,10 +104,16 @@ class PISGradNet(torch.nn.Module):
 
 
 def _unwrap(module):
-    """PicardSolution-like wrappers keep the network in `.model` (picard/solution.py:313-325)."""
-    while hasattr(module, "model") and isinstance(module.model, torch.nn.Module):
-        module = module.model
-    return module
+    """The network inside the reference's solution wrappers: PicardSolution keeps it in `.model`
+    (picard/solution.py:313-325), PicardSolutionGradientWrapper / ...HessianWrapper keep the
+    PicardSolution in `.solution` (picard/solution_jac.py:124-126, 219-226)."""
+    while True:
+        inner = getattr(module, "model", None)
+        if not isinstance(inner, torch.nn.Module):
+            inner = getattr(module, "solution", None)
+        if not isinstance(inner, torch.nn.Module):
+            return module
+        module = inner
 
 
 class DeviceNet:

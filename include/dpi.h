@@ -170,7 +170,10 @@ int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M,
  * that is the first path chunk's Philox + K-step Euler-Maruyama rollout and the baseline rows
  * (data.py:471-527, 899-926 up to the network call); for the fused-kernel nets it is a no-op.  Same
  * arguments as dpi_label_moments (after dpi_point_baseline on the same workspace); the matching
- * dpi_label_moments call then passes flags | DPI_PREPARED. */
+ * dpi_label_moments call then passes flags | DPI_PREPARED.  The library records the prepare
+ * call's arguments per workspace (host side); a DPI_PREPARED call whose arguments (points pointer,
+ * n, M, K, seed, epoch, point_base, MC range, flags, workspace size) differ, or that has no prepare
+ * on its workspace, fails with DPI_ERR_ARG.  Each prepare is consumed by one prepared call. */
 int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                       uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, void* ws,
                       size_t ws_bytes, void* stream);

@@ -11,7 +11,7 @@ from torch.utils.data import DataLoader
 
 from deeppicarditeration_amd import dataset as D
 from deeppicarditeration_amd.data import OnlineDataGenerator
-from picard_datamodule import PicardDataModuleStandIn
+from picard_datamodule import PicardDataModuleStandIn, reference_data_cfg
 
 NX = 3
 
@@ -116,6 +116,7 @@ class _SurfaceOnly(OnlineDataGenerator):
 
     def __init__(self, equation):
         self.equation = equation
+        self.max_points_per_call = None
 
 
 def test_get_dataset_details_reads_the_whole_generator_surface():
@@ -126,8 +127,9 @@ def test_get_dataset_details_reads_the_whole_generator_surface():
     for exact, grad, hess, name, dim in [(False, True, False, "u_ux", 1 + NX), (False, True, True, "u_ux_uh", 1 + NX + NX * NX),
                                          (True, True, False, "u_ux", 1 + NX), (True, False, False, "u", 1),
                                          (False, False, False, "u", 1), (True, True, True, "u_ux_uh", 1 + NX + NX * NX)]:
-        dm = PicardDataModuleStandIn(g, NX, data_size=64, batch_size=8, n_batch_buffer=2, exact=exact,
-                                     generate_gradients=grad, generate_hessians=hess)
+        dm = PicardDataModuleStandIn.__new__(PicardDataModuleStandIn)  # no generator construction
+        dm.data_generator, dm.equation, dm.data_cfg = g, g.equation, reference_data_cfg(EXACT=exact)
+        dm.generate_gradients, dm.generate_hessians = grad, hess
         fn, d, nm = dm.get_dataset_details()
         assert (d, nm) == (dim, name)
         ds = fn(64, 2, 8)  # building the dataset draws nothing

@@ -584,3 +584,31 @@ def test_side_stream_preparation_equals_labels(kind):
     for y in got:
         tx, pb = ref.gen.sample_t_and_x(16)
         assert torch.equal(y, ref.labels(tx, pb))
+
+
+@pytest.mark.gpu
+def test_prepared_moments_check_the_prepare_call():
+    """include/dpi.h DPI_PREPARED contract: a prepared moments call whose points, counters or MC
+    range differ from the dpi_label_prepare call on its workspace, or that has no prepare (a second
+    prepared call consumes nothing), fails with DPI_ERR_ARG instead of returning labels built from
+    another batch's rollout; the matching call succeeds."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    torch.manual_seed(4)
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    net = dpi.PISGradNet(hidden_shapes=[32] * 2, dim=100, g0=eq.g, T=1.0)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=3, seed=3)
+    tx, pb = gen.sample_t_and_x(4)
+    ws = gen.point_baseline(tx)
+    gen.label_prepare(tx, pb, 128, 0, 128, L.DPI_BOTH, ws)
+    with pytest.raises(RuntimeError, match="DPI_PREPARED"):
+        gen.label_moments(tx, pb + 1, 128, 0, 128, L.DPI_BOTH | L.DPI_PREPARED, ws)
+    gen.label_prepare(tx, pb, 128, 0, 128, L.DPI_BOTH, ws)
+    mom = gen.label_moments(tx, pb, 128, 0, 128, L.DPI_BOTH | L.DPI_PREPARED, ws)
+    with pytest.raises(RuntimeError, match="DPI_PREPARED"):  # consumed
+        gen.label_moments(tx, pb, 128, 0, 128, L.DPI_BOTH | L.DPI_PREPARED, ws)
+    ref = gen.label_moments(tx, pb, 128, 0, 128, L.DPI_BOTH, gen.point_baseline(tx))
+    torch.cuda.synchronize()
+    assert torch.equal(mom, ref)

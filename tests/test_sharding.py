@@ -269,3 +269,53 @@ def test_four_rank_gloo_labels_equal_single_rank():
         p.join(timeout=60)
     for r in range(4):
         assert res[r].tobytes() == single.tobytes(), r
+
+
+def _worker_non_pow2(rank, world, port, q):
+    """M = 384 over 2 ranks: 3 blocks of 64 paths per rank (not a power of two)."""
+    import warnings
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeppicarditeration_amd.sharding import ShardBitIdentityWarning, ShardedLabeler
+    eq, net, tx = _problem()
+    gen = OracleGen(eq, net)
+    gen.n_estimate_terminal = gen.n_estimate_integral = 384
+    lab = ShardedLabeler(gen, rank=rank, world=world)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        y = lab.labels(tx, 0)
+    q.put((rank, y.numpy(), [issubclass(x.category, ShardBitIdentityWarning) for x in w]))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_non_power_of_two_blocks_warns():
+    """M / (64 G) not a power of two: every rank warns that the labels lose bit-identity with the
+    single-GPU call, and the labels still agree with it to fp32 rounding."""
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    g1 = OracleGen(eq, net)
+    g1.n_estimate_terminal = g1.n_estimate_integral = 384
+    single = ShardedLabeler(g1, 0, 1).labels(tx, 0).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_non_pow2, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (y, w) for r, y, w in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        y, w = res[r]
+        assert any(w), f"rank {r} did not warn"
+        np.testing.assert_allclose(y, single, rtol=1e-5, atol=1e-6)
+
+
+def test_power_of_two_shards_do_not_warn():
+    import warnings
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        for G in (1, 2, 4, 8):
+            for r in range(G):
+                ShardedLabeler(None, r, G).shard(4096)

@@ -15,11 +15,12 @@ for w in $what; do
     run 900 $out/gpu_tests.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
   bench)
     run 300 $out/bench_burgers.log python bench.py
+    run 300 $out/bench_burgers_cfg3.log python bench.py --workload burgers_cfg3
     run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
     run 300 $out/bench_gbm.log python bench.py --workload gbm --steps 20 --warmup 3
     run 300 $out/bench_gbm_hess.log python bench.py --workload gbm_hess --steps 10 --warmup 2 ;;
   trace)
-    for wl in burgers gbm gbm_hess; do
+    for wl in burgers burgers_cfg3 gbm gbm_hess; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_$wl -o trace --output-format csv -- \
         python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_$wl.log 2>&1
     done
@@ -35,12 +36,12 @@ for w in $what; do
   counters)
     timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
   pmc)
-    for wl in burgers gbm gbm_hess; do
+    for wl in burgers burgers_cfg3 gbm gbm_hess; do
       timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
         --kernel-include-regex k_paths -d $out/pmc_valu_$wl -o pmc --output-format csv -- \
         python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu_$wl.log 2>&1
     done
-    for wl in burgers hjb gbm gbm_hess; do
+    for wl in burgers burgers_cfg3 hjb gbm gbm_hess; do
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm|k_reduce" -d $out/pmc_${wl}_$c -o pmc \
           --output-format csv -- python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_${wl}_$c.log 2>&1

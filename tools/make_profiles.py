@@ -11,7 +11,7 @@ from pathlib import Path
 
 src, tag = Path(sys.argv[1]), sys.argv[2]
 dst = Path(__file__).resolve().parents[1] / "profiles"
-for wl in ("burgers", "hjb", "gbm", "gbm_hess", "hjb_onestream"):
+for wl in ("burgers", "burgers_cfg3", "hjb", "gbm", "gbm_hess", "hjb_onestream"):
     f = src / f"trace_{wl}" / "trace_kernel_stats.csv"
     if f.exists():
         rows = list(csv.DictReader(open(f)))
@@ -29,7 +29,7 @@ for wl in ("burgers", "hjb", "gbm", "gbm_hess", "hjb_onestream"):
 # of the anchor kernel (k_paths, or k_pis_final for the PISGradNet chain, whose prepare-stream rollout
 # runs as several grids per call); the bytes of every
 # kernel of the call (rollout, GEMM chain, final, reduce) are summed.
-ANCHOR = {"burgers": "dpi::k_paths", "gbm": "dpi::k_paths", "gbm_hess": "dpi::k_paths", "hjb": "dpi::k_pis_final"}
+ANCHOR = {"burgers": "dpi::k_paths", "burgers_cfg3": "dpi::k_paths", "gbm": "dpi::k_paths", "gbm_hess": "dpi::k_paths", "hjb": "dpi::k_pis_final"}
 for wl, anchor in ANCHOR.items():
     pmc = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -62,7 +62,7 @@ for wl, anchor in ANCHOR.items():
 # and the bench's u = 0 noise-floor launch), averaged over dispatches.  SQ_ACTIVE_INST_VALU is in
 # quad-cycles summed over all SIMDs (1024); GRBM_GUI_ACTIVE is summed over the 8 XCDs.
 N_SIMD, N_XCD = 1024, 8
-for wl in ("burgers", "gbm", "gbm_hess"):
+for wl in ("burgers", "burgers_cfg3", "gbm", "gbm_hess"):
     f = src / f"pmc_valu_{wl}" / "pmc_counter_collection.csv"
     if not f.exists() and wl == "burgers":
         f = src / "pmc_valu" / "pmc_counter_collection.csv"
