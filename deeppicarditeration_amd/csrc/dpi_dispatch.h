@@ -18,6 +18,9 @@ struct dpi_net_s {
   NetPisDev pis;
   void* blob = nullptr;
   int n_in = 0;
+  int precision = -1;     // DPI_GEMM_* for this net (dpi_net_set_precision); -1: the process-wide mode
+  bool finite = true;     // every uploaded parameter finite
+  int* status = nullptr;  // device word, sticky: DPI_STATUS_* bits the label reductions set (dpi_net_status)
 };
 
 // ---- dispatch over (equation, network shape)

@@ -60,10 +60,19 @@ __device__ __forceinline__ float clip_label(float v, float bound) {
   return v != v ? v : fminf(fmaxf(v, -bound), bound);
 }
 
+// Range guard: a label sum that is not finite while the network's parameters are (status != null
+// only then) means the network evaluation left its number format — fp16's 65,504 in the split
+// storage of the PISGradNet pipeline, or fp32's range — where the fp64 reference would not.  The
+// lane stores DPI_STATUS_NONFINITE into the net's sticky status word (a plain vector store: any
+// number of writers store the same value); the host reads it with dpi_net_status.
+__device__ __forceinline__ void flag_nonfinite(int* status, float s) {
+  if (status && !__builtin_isfinite(s)) *(volatile int*)status = DPI_STATUS_NONFINITE;
+}
+
 __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partial, int n, int F, int nbp,
                                                 float* __restrict__ moments, const float* __restrict__ gx,
                                                 float invM, int add_g, float bound, float* __restrict__ y,
-                                                int ystride) {
+                                                int ystride, int* status) {
   // a wave per (point, column): reading the slab's lines from several XCDs costs only duplicate
   // fetches of a 0.9 MB slab, while one workgroup per point serialised the columns (14 vs 4.4 us)
   const int i = blockIdx.x, R = slab_row(F);
@@ -71,6 +80,7 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
   if (c >= 2 * F) return;
   const float s = tree_sum(partial + (size_t)i * nbp * R + c, nbp, (size_t)R);
   if ((threadIdx.x & 63) == 0) {
+    if (c < F) flag_nonfinite(status, s);  // the label sums (a sum of squares may overflow alone)
     moments[(size_t)i * 2 * F + c] = s;
     if (y && c < F) {
       float v = s * invM;
@@ -84,12 +94,13 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
 // the canonical tree over blocks.
 __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int C, int nbp,
                                                      float* __restrict__ hsum, float invM, float bound,
-                                                     float* __restrict__ y, int ystride, int yoff) {
+                                                     float* __restrict__ y, int ystride, int yoff, int* status) {
   const int i = blockIdx.y;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
   const float s = tree_sum(hpart + (size_t)i * nbp * C + c, nbp, (size_t)C);
   if ((threadIdx.x & 63) == 0) {
+    flag_nonfinite(status, s);
     if (hsum) hsum[(size_t)i * C + c] = s;
     if (y) y[(size_t)i * ystride + yoff + c] = clip_label(s * invM, bound);
   }
@@ -101,7 +112,7 @@ __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ h
 // binary tree over 64 zero-padded leaves, so the results are bitwise those of k_reduce_hess.
 __global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__ hpart, int n, int C, int nbp,
                                                        float* __restrict__ hsum, float invM, float bound,
-                                                       float* __restrict__ y, int ystride, int yoff) {
+                                                       float* __restrict__ y, int ystride, int yoff, int* status) {
   const int i = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   const float* p = hpart + (size_t)i * nbp * C + c;
@@ -112,6 +123,7 @@ __global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__
   for (int w = 1; w < 64; w <<= 1)
 #pragma unroll
     for (int b = 0; b < 64; b += 2 * w) v[b] = v[b] + v[b + w];
+  flag_nonfinite(status, v[0]);
   if (hsum) hsum[(size_t)i * C + c] = v[0];
   if (y) y[(size_t)i * ystride + yoff + c] = clip_label(v[0] * invM, bound);
 }
@@ -241,6 +253,7 @@ int dpi_last_error(char* buf, size_t len) {
 }
 
 int dpi_problem_destroy(dpi_problem p);
+int dpi_net_destroy(dpi_net net);
 
 static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
   auto* p = new dpi_problem_s();
@@ -343,12 +356,44 @@ int dpi_problem_destroy(dpi_problem p) {
   return 0;
 }
 
+// The net's sticky status word (DPI_STATUS_*), zeroed; and whether every parameter is finite.
+static int net_init_status(dpi_net_s* n, const float* params, size_t n_params) {
+  n->finite = true;
+  for (size_t i = 0; i < n_params; ++i)
+    if (!std::isfinite(params[i])) {
+      n->finite = false;
+      break;
+    }
+  HIPCHK(hipMalloc(&n->status, 256));
+  HIPCHK(hipMemset(n->status, 0, 256));
+  return 0;
+}
+
 int dpi_net_create_zero(dpi_net* out) {
   if (!out) return fail(DPI_ERR_ARG, "null out");
   auto* n = new dpi_net_s();
   std::memset(&n->d, 0, sizeof(n->d));
-  n->d.kind = 0;
+  n->d.kind = 0;  // u = 0 cannot overflow: no status word (creation stays host-only)
   *out = n;
+  return 0;
+}
+
+int dpi_net_set_precision(dpi_net net, int mode) {
+  if (!net || mode < -1 || mode > DPI_GEMM_AUTO) return fail(DPI_ERR_ARG, "net_set_precision: bad arguments");
+  net->precision = mode;
+  return 0;
+}
+
+int dpi_net_status(dpi_net net, int clear, void* stream, int* status) {
+  if (!net || !status) return fail(DPI_ERR_ARG, "net_status: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  int v = 0;
+  if (net->status) {
+    HIPCHK(hipMemcpyAsync(&v, net->status, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (clear && v) HIPCHK(hipMemsetAsync(net->status, 0, sizeof(int), st));
+  }
+  *status = v;
   return 0;
 }
 
@@ -462,6 +507,10 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
       n->d.WU[l] = u32(oWU[l]);
       n->d.wus[l] = wus[l];
     }
+  }
+  if (int rc = net_init_status(n, params, n_params)) {
+    dpi_net_destroy(n);
+    return rc;
   }
   *out = n;
   return 0;
@@ -682,6 +731,10 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
   n->n_in = 1 + nx;
   n->d.kind = 2;
   n->pis = pd;
+  if (int rc = net_init_status(n, params, n_params)) {
+    dpi_net_destroy(n);
+    return rc;
+  }
   *out = n;
   return 0;
 }
@@ -689,6 +742,7 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
 int dpi_net_destroy(dpi_net net) {
   if (!net) return 0;
   if (net->blob) (void)hipFree(net->blob);
+  if (net->status) (void)hipFree(net->status);
   delete net;
   return 0;
 }
@@ -792,8 +846,10 @@ static int gemm_mode() {
   }
   return g_gemm_mode;
 }
-static bool mlp_split() { return gemm_mode() != DPI_GEMM_F32; }
-static bool pis_x3(const NetPisDev&) { return gemm_mode() != DPI_GEMM_F32; }
+static int net_mode(dpi_net net) { return (net && net->precision >= 0) ? net->precision : gemm_mode(); }
+static bool mlp_split(dpi_net net) { return net_mode(net) != DPI_GEMM_F32; }
+static bool pis_x3(dpi_net net) { return net_mode(net) != DPI_GEMM_F32; }
+static int* net_status(dpi_net net) { return (net && net->finite) ? net->status : nullptr; }
 
 extern "C" int dpi_set_gemm_precision(int mode) {
   if (mode != DPI_GEMM_F32 && mode != DPI_GEMM_F16X3 && mode != DPI_GEMM_AUTO)
@@ -1074,7 +1130,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
   if (rc) return rc;
   float* rows = (float*)(b + w.rows);
   float* fb = (float*)(b + w.fb);
-  const bool x3 = pis_x3(net->pis);
+  const bool x3 = pis_x3(net);
   const PisRows L = pis_rows_layout(net->pis, x3);
   const int G = n * a.nbp, GC = std::max(1, (w.rows_cap - n) / P);
   const float dt = a.td_dt;
@@ -1202,7 +1258,7 @@ static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.point_base = point_base;
   a.order = path_order();
-  a.split = mlp_split() ? 1 : 0;
+  a.split = mlp_split(net) ? 1 : 0;
   a.td_dt = p->td_dt;
   return 0;
 }
@@ -1229,7 +1285,8 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   }
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
-                     (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F);
+                     (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F,
+                     net_status(net));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1414,7 +1471,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.c3q = DPI_TAG_SDGD | (epoch << 8);
   a.c3h1 = DPI_TAG_HTERM | (epoch << 8);
   a.c3h2 = DPI_TAG_HINT | (epoch << 8);
-  a.split = mlp_split() ? 1 : 0;  // fp16-split tangent sweeps (mlp_hdiag_split) unless DPI_GEMM_F32
+  a.split = mlp_split(net) ? 1 : 0;  // fp16-split tangent sweeps (mlp_hdiag_split) unless DPI_GEMM_F32
   a.point_base = point_base;
   a.hpart = (float*)(b + base);
   hipStream_t st = (hipStream_t)stream;
@@ -1424,13 +1481,13 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
-                     1.0f / (float)M, 1, bound, y, F + C);
+                     1.0f / (float)M, 1, bound, y, F + C, net_status(net));
   if (nbp <= 64)
     hipLaunchKernelGGL(k_reduce_hess64, dim3((C + 255) / 256, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
-                     1.0f / (float)M, bound, y, F + C, F);
+                     1.0f / (float)M, bound, y, F + C, F, net_status(net));
   else
     hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
-                     1.0f / (float)M, bound, y, F + C, F);
+                     1.0f / (float)M, bound, y, F + C, F, net_status(net));
   HIPCHK(hipGetLastError());
   return 0;
 }

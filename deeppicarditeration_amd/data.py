@@ -19,6 +19,7 @@ Differences from the reference, by design:
 `estimate_delta_t > 0` selects the reference's TD estimators (data.py:1209-1213) on the device
 (every network kind).
 """
+import warnings
 from typing import Union
 
 import torch
@@ -35,6 +36,11 @@ def _ptr(t):
 
 def _stream(device):
     return _lib.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class SplitRangeWarning(RuntimeWarning):
+    """A network's fp16-split evaluation left fp16's range: its labels are recomputed, and the
+    generator's later calls made, with exact-fp32 MFMA (DPI_GEMM_F32) for that network."""
 
 
 def _hessian_approximation(cfg):
@@ -111,6 +117,13 @@ class OnlineDataGenerator:
         self.sdgd_v = sdgd_v
         self._configure_problem()
         self._ws = None
+        # Range guard of the label calls (include/dpi.h dpi_net_status): after each call the net's
+        # status word says whether a label came out non-finite from finite weights — the network
+        # evaluation overflowed fp16 (split storage) or fp32.  Split: the call is recomputed in
+        # exact fp32 and the net stays fp32 (SplitRangeWarning); fp32 already: DPIError.  Never a
+        # silent inf / NaN label.  One stream synchronisation per call; False skips the check.
+        self.range_check = True
+        self._fp32_fallback = False
         # Points per generator call of the dataset surface (None: unbounded).  The reference sizes
         # its calls by probing GPU memory (picard/memory.py:95-171): a dataset whose calls exceed
         # this cap raises torch.cuda.OutOfMemoryError, which those probes read as "does not fit",
@@ -373,7 +386,37 @@ class OnlineDataGenerator:
         return out
 
     # ------------------------------------------------------------------ internals
+    def range_status(self, clear=True):
+        """DPI_STATUS_* bits set by the label calls on this generator's net since the last clear."""
+        return self.net.status(_stream(self._device), clear)
+
+    def _guarded(self, call):
+        """Run a label call; on a DPI_STATUS_NONFINITE flag switch the net to exact fp32 and run it
+        again (same points and counters), or raise if it already ran in fp32."""
+        y = call()
+        # no check inside a hipGraph capture (a synchronisation there would invalidate the capture);
+        # the flag stays set and the next checked call on this net reports it
+        if not self.range_check or torch.cuda.is_current_stream_capturing() or \
+                not (self.range_status() & _lib.DPI_STATUS_NONFINITE):
+            return y
+        if self._fp32_fallback:
+            raise _lib.DPIError("label call gave non-finite labels from a network with finite parameters in exact "
+                                "fp32: the network's values exceed fp32's range")
+        warnings.warn("the fp16-split evaluation of this network left fp16's range (|activation| > 65504); its "
+                      "labels are recomputed, and this generator's later calls run, with exact-fp32 MFMA",
+                      SplitRangeWarning, stacklevel=3)
+        self.use_fp32()
+        return self._guarded(call)
+
+    def use_fp32(self):
+        """Evaluate this generator's network with exact-fp32 MFMA from now on (dpi_net_set_precision)."""
+        self.net.set_precision(_lib.DPI_GEMM_F32)
+        self._fp32_fallback = True
+
     def _generate_hess(self, tx, pb, bound):
+        return self._guarded(lambda: self._generate_hess_once(tx, pb, bound))
+
+    def _generate_hess_once(self, tx, pb, bound):
         if self.n_estimate_terminal != self.n_estimate_integral:
             raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
         n, nx, M = tx.shape[0], self.equation.nx, self.n_estimate_integral
@@ -394,6 +437,9 @@ class OnlineDataGenerator:
         return tx
 
     def _generate(self, tx, pb, flags, bound=None):
+        return self._guarded(lambda: self._generate_once(tx, pb, flags, bound))
+
+    def _generate_once(self, tx, pb, flags, bound=None):
         MT, MI = self.n_estimate_terminal, self.n_estimate_integral
         if MT == MI or flags != _lib.DPI_BOTH:
             # one C-ABI call: baseline + fused rollout/label kernel + block reduce/finalize

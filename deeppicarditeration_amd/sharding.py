@@ -65,7 +65,35 @@ class ShardedLabeler:
         dist.all_gather_into_tensor(flat, x, group=self.group)
         return self.gen.sums_reduce(flat.view((self.world,) + tuple(x.shape)))
 
+    def _guarded(self, call):
+        """The generator's range guard (OnlineDataGenerator._guarded) across ranks: any rank's flag
+        is every rank's (a one-word all-reduce), so all ranks recompute in fp32 together."""
+        gen = self.gen
+        y = call()
+        if not getattr(gen, "range_check", False) or torch.cuda.is_current_stream_capturing():
+            return y
+        flag = gen.range_status()
+        if self.world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([float(flag)], device=y.device if dist.get_backend(self.group) != "gloo" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            flag = int(t.item())
+        if not flag:
+            return y
+        from . import _lib
+        if gen._fp32_fallback:
+            raise _lib.DPIError("non-finite labels from a network with finite parameters in exact fp32")
+        import warnings
+        from .data import SplitRangeWarning
+        warnings.warn("the fp16-split evaluation left fp16's range: labels recomputed in exact fp32", SplitRangeWarning,
+                      stacklevel=3)
+        gen.use_fp32()
+        return self._guarded(call)
+
     def labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
+        return self._guarded(lambda: self._labels_hessians(tx, point_base, on_moments_begin, on_moments_end))
+
+    def _labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients_and_hessians for tx with this rank's MC shard (n, 1 + nx + nx^2);
         identical on every rank.  Exchange: the (n, 2, 1+nx) moments and (n, nx^2) Hessian sums."""
         M = self.gen.n_estimate_integral
@@ -190,7 +218,11 @@ class ShardedLabeler:
         return y
 
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
-        """generate_with_gradients for tx with this rank's MC shard; identical y on every rank."""
+        """generate_with_gradients for tx with this rank's MC shard; identical y on every rank
+        (range-guarded like the generator's calls when gen.range_check)."""
+        return self._guarded(lambda: self._labels(tx, point_base, flags, on_moments_begin, on_moments_end))
+
+    def _labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         from . import _lib
         flags = _lib.DPI_BOTH if flags is None else flags
         M = self.gen.n_estimate_integral

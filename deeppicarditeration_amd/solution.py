@@ -129,6 +129,17 @@ class DeviceNet:
         except Exception:
             pass
 
+    def set_precision(self, mode):
+        """Per-network GEMM precision (include/dpi.h dpi_net_set_precision; -1 = process-wide)."""
+        _lib.check(_lib.load().dpi_net_set_precision(self.handle, int(mode)), "dpi_net_set_precision")
+
+    def status(self, stream, clear=True):
+        """The sticky DPI_STATUS_* word of the label reductions on this net (synchronises `stream`)."""
+        v = _lib.c_int(0)
+        _lib.check(_lib.load().dpi_net_status(self.handle, 1 if clear else 0, stream, _lib.ctypes.byref(v)),
+                   "dpi_net_status")
+        return v.value
+
     @classmethod
     def from_module(cls, module, n_in: int):
         lib = _lib.load()

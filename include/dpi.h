@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 1
+#define DPI_ABI_VERSION 2
 
 /* error codes */
 #define DPI_OK 0
@@ -134,6 +134,21 @@ int dpi_net_destroy(dpi_net net);
 #define DPI_GEMM_F16X3 1
 #define DPI_GEMM_AUTO 2
 int dpi_set_gemm_precision(int mode);
+
+/* Per-network override of the GEMM precision (-1: follow dpi_set_gemm_precision).  The host layer
+ * switches one network to DPI_GEMM_F32 when its split evaluation leaves fp16's range (below). */
+int dpi_net_set_precision(dpi_net net, int mode);
+
+/* Range guard.  Every label reduction of a call on `net` (dpi_label_moments*, the Hessian sums)
+ * sets DPI_STATUS_NONFINITE in the net's sticky device status word when a label sum (not a sum of
+ * squares, whose overflow leaves the labels intact) is not finite
+ * while every parameter of the net is finite: the network evaluation overflowed its number format
+ * (fp16's 65,504 in the fp16-split PISGradNet storage, or fp32's range), where the fp64 reference
+ * would not.  (Non-finite parameters give non-finite labels as in the reference, unflagged.)
+ * dpi_net_status copies the word to *status after the work queued on `stream` (a synchronisation)
+ * and, with clear != 0, resets it.  Replaces no reference interface. */
+#define DPI_STATUS_NONFINITE 1
+int dpi_net_status(dpi_net net, int clear, void* stream, int* status);
 
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
 size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);

@@ -233,6 +233,15 @@ def main(only=None):
     run_case("ou_mlp16_K2", "OUProcessEquation", ou, "mlp", {"neurons": [16, 16]}, 3, 64, 2, 5, workdir=wd)
     run_case("ou_mlp128x4_K3", "OUProcessEquation", ou, "mlp", {"neurons": [128] * 4}, 2, 64, 3, 9, workdir=wd)
     run_case("ou_zero_K1", "OUProcessEquation", ou, "mlp", {"neurons": [8]}, 3, 64, 1, 2, workdir=wd, zero=True)
+    # range / precision stress of the fp16-split default: every network parameter scaled by 8 and 32
+    run_case("cha_mlp128x4_ws8_K3", "Cha", cha, "mlp", {"neurons": [128] * 4}, 2, 64, 3, 41, workdir=wd,
+             weight_scale=8.0)
+    run_case("cha_mlp128x4_ws32_K3", "Cha", cha, "mlp", {"neurons": [128] * 4}, 2, 64, 3, 42, workdir=wd,
+             weight_scale=32.0)
+    run_case("ou_pis32_ws8_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 64, 2, 43, workdir=wd,
+             weight_scale=8.0)
+    run_case("ou_pis32_ws32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 64, 2, 44, workdir=wd,
+             weight_scale=32.0)
     # Fully-nonlinear case_1 (GBM): SDGD v=100 and full-Hessian (v=0), MLP 3x16
     run_case("gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 3, 64, 2, 3,
              v=100, workdir=wd)

@@ -66,6 +66,9 @@ def test_host_side_argument_errors_without_gpu():
     assert lib.dpi_problem_set_estimate_delta_t(h, 0.25) == 0 and lib.dpi_problem_set_estimate_delta_t(h, 0.0) == 0
     assert lib.dpi_problem_set_hessian_approximation(h, 256) == _lib.DPI_ERR_ARG
     assert lib.dpi_set_gemm_precision(7) == _lib.DPI_ERR_ARG
+    assert lib.dpi_net_set_precision(None, 0) == _lib.DPI_ERR_ARG
+    st = _lib.c_int(0)
+    assert lib.dpi_net_status(None, 1, None, _lib.ctypes.byref(st)) == _lib.DPI_ERR_ARG
     assert lib.dpi_net_destroy(n) == 0 and lib.dpi_problem_destroy(h) == 0
 
 

@@ -76,3 +76,44 @@ def test_gbm_config4_full_size():
     onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
                  ["ELU"] * 3)
     _check(gen, O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy()), onet, n, M, K, v=v)
+
+
+def test_gbm_hessian_labels_config4_full_size():
+    """Malliavin-weight Hessian labels (generate_with_gradients_and_hessians, picard/data.py:1220-1223;
+    _double estimators :823-897, :1153-1201) at BASELINE configs[4] size: 64 points x 1024 paths,
+    K = 50, 3 x 64 ELU network.  Bitwise-reproducible sums, 2 / 4 / 8 MC shards + dpi_sums_reduce
+    equal to the single call bit for bit, moments + finalize equal to the one-call labels, and the
+    first and last point (value, gradient and the 100 x 100 Hessian block) within rel-L2 1e-4 of
+    the fp64 oracle on the same counters."""
+    import deeppicarditeration_amd as dpi
+    from oracle import dpi_oracle as O
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    torch.manual_seed(3)
+    net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+    n, M, K = 64, 1024, 50
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    ws = gen.point_baseline(tx, hessians=True)
+    mom, hs = gen.label_moments_hessians(tx, 0, M, 0, M, ws)
+    mom2, hs2 = gen.label_moments_hessians(tx, 0, M, 0, M, ws)
+    assert torch.equal(mom, mom2) and torch.equal(hs, hs2)
+    for G in (2, 4, 8):
+        parts = [gen.label_moments_hessians(tx, 0, M, r * M // G, (r + 1) * M // G, ws) for r in range(G)]
+        assert torch.equal(gen.sums_reduce(torch.stack([p[0] for p in parts])), mom), G
+        assert torch.equal(gen.sums_reduce(torch.stack([p[1] for p in parts])), hs), G
+    y = gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"))
+    assert torch.equal(y, gen.generate_with_gradients_and_hessians(tx, point_base=0))
+    y = y.cpu().double().numpy()
+    assert np.isfinite(y).all() and y.shape == (n, 1 + 100 + 100 * 100)
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
+                 ["ELU"] * 3)
+    oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+    txh = tx.cpu().double().numpy()
+    for i in (0, n - 1):
+        ref = O.labels_grad_hess(oeq, onet, txh[i:i + 1], M, K, 1, 1, i, m_chunk=256)
+        ev, eg, eh = (_rel(y[i:i + 1, :1], ref[:, :1]), _rel(y[i:i + 1, 1:101], ref[:, 1:101]),
+                      _rel(y[i:i + 1, 101:], ref[:, 101:]))
+        print(f"point {i}: value {ev:.2e} grad {eg:.2e} hessian {eh:.2e}")
+        assert ev < TOL and eg < TOL and eh < TOL, (i, ev, eg, eh)

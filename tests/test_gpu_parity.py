@@ -26,7 +26,7 @@ from golden_util import CASES, delta_t, load, oracle_equation, oracle_net, t_fac
 from gpu_util import generator, product_equation, product_module, rel_l2_parts  # noqa: E402
 from oracle import dpi_oracle as O  # noqa: E402
 
-SUPPORTED = list(CASES)
+SUPPORTED = [c for c in CASES if "_ws" not in c]  # weight-scaled fixtures: tests/test_gpu_range.py, both modes
 
 
 @pytest.mark.parametrize("case", SUPPORTED)

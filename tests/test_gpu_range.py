@@ -1,0 +1,158 @@
+"""Range and precision of the fp16-split MFMA default under large weights,
+with the fp64 oracle as the judge (VERDICT r2 "weak" 2): every network parameter multiplied by s
+(tests/golden/make_golden.py's weight_scale), both GEMM modes, and the range guard
+(include/dpi.h dpi_net_status) where the split storage overflows.
+
+Measured bound (tools/probe_range.py, profiles/r03b_probe_range.jsonl): the fused MLPs stay within
+rel-L2 1e-4 of the oracle for s <= 32 (Cha 4 x 128: labels up to 2e10) in both modes; GBM 3 x 64's
+SDGD labels lose accuracy past s = 16 in BOTH modes (fp32's own conditioning of f = ... |u_ii| terms at
+labels ~1e5, not the split); the PISGradNet split storage overflows fp16 past s ~ 12 (labels ~1e21),
+where the guard recomputes in fp32."""
+import warnings
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dpi_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(params=["auto", "f32"])
+def mode(request):
+    from deeppicarditeration_amd import _lib as L
+    L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO if request.param == "auto" else L.DPI_GEMM_F32), "prec")
+    yield request.param
+    L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "prec")
+
+
+def _scaled(net, s):
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(s)
+    return net
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _mlp_oracle(net):
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    return O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
+                 ["ELU"] * (len(lin) - 1))
+
+
+@pytest.mark.parametrize("eqname, widths, scale", [("cha", [128] * 4, 8.0), ("cha", [128] * 4, 32.0),
+                                                   ("cha", [128] * 4, 1 / 32), ("gbm", [64] * 3, 8.0),
+                                                   ("gbm", [64] * 3, 16.0)])
+def test_scaled_mlp_vs_oracle(mode, eqname, widths, scale):
+    import deeppicarditeration_amd as dpi
+    torch.manual_seed(3)
+    if eqname == "cha":
+        eq, oeq, v = dpi.Cha(100, 1.0, 5.0, 1.0), O.Cha(100, 1.0, 5.0, 1.0), 0
+    else:
+        eq = dpi.GBMEquationComplexExact(100)
+        oeq, v = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy()), 100
+    net = _scaled(dpi.construct_mlp(101, 1, widths, ["ELU"] * len(widths), None), scale)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                  n_estimate_integral=256, n_euler_steps=10, seed=1,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": v}} if v else None)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # no fallback needed: the fused MLP stays in range
+        tx, y = gen.sample_with_gradients(2)
+    ref = O.labels_grad(oeq, _mlp_oracle(net), tx.cpu().double().numpy(), 256, 10, 1, 1, 0, v=v)
+    y = y.cpu().double().numpy()
+    ev, eg = _rel(y[:, :1], ref[:, :1]), _rel(y[:, 1:], ref[:, 1:])
+    print(f"{eqname} x{scale} {mode}: max|label| {np.abs(ref).max():.2e} value {ev:.2e} grad {eg:.2e}")
+    assert ev < TOL and eg < TOL
+
+
+def _pis(scale):
+    import deeppicarditeration_amd as dpi
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(7)
+    net = _scaled(dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0), scale)
+    with torch.no_grad():
+        net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=10, seed=2)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    return gen, oeq, onet
+
+
+@pytest.mark.parametrize("scale", [8.0, 32.0])
+def test_scaled_pisgradnet_vs_oracle(mode, scale):
+    """PISGradNet 4 x 512: at 8x both modes match the oracle directly; at 32x the split storage
+    overflows fp16 (labels ~1e29) and the range guard recomputes the call in exact fp32 with a
+    SplitRangeWarning — never a silent inf / NaN label."""
+    from deeppicarditeration_amd.data import SplitRangeWarning
+    gen, oeq, onet = _pis(scale)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        tx, y = gen.sample_with_gradients(2)
+    fell_back = any(issubclass(x.category, SplitRangeWarning) for x in w)
+    assert fell_back == (mode == "auto" and scale == 32.0), [str(x.message) for x in w]
+    assert bool(torch.isfinite(y).all())
+    ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 10, 2, 1, 0)
+    y = y.cpu().double().numpy()
+    ev, eg = _rel(y[:, :1], ref[:, :1]), _rel(y[:, 1:], ref[:, 1:])
+    print(f"pis x{scale} {mode}: max|label| {np.abs(ref).max():.2e} value {ev:.2e} grad {eg:.2e} fallback {fell_back}")
+    assert ev < TOL and eg < TOL
+    if fell_back:  # the generator stays in fp32: no further flag, no further warning
+        with warnings.catch_warnings():
+            warnings.simplefilter("error")
+            _, y2 = gen.sample_with_gradients(2)
+        assert bool(torch.isfinite(y2).all()) and gen.range_status() == 0
+
+
+def test_fp32_overflow_raises():
+    """Labels beyond fp32's range from finite weights: a loud DPIError (after the fp32 retry)."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd._lib import DPIError
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    torch.manual_seed(3)
+    net = _scaled(dpi.construct_mlp(101, 1, [32, 32], ["ELU"] * 2, None), 1e13)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                  n_estimate_integral=64, n_euler_steps=2, seed=1)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with pytest.raises(DPIError, match="fp32"):
+            gen.sample_with_gradients(2)
+
+
+def test_nan_parameters_are_not_flagged():
+    """NaN weights give NaN labels as in the reference (torch propagates them): no flag, no error."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    torch.manual_seed(0)
+    net = dpi.construct_mlp(101, 1, [32, 32], ["ELU", "ELU"], None)
+    with torch.no_grad():
+        net[0].weight[0, 0] = float("nan")
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                  n_estimate_integral=64, n_euler_steps=2, seed=1)
+    _, y = gen.sample_with_gradients(2)
+    assert bool(torch.isnan(y).any()) and gen.range_status() == 0
+
+
+@pytest.mark.parametrize("case", ["cha_mlp128x4_ws8_K3", "cha_mlp128x4_ws32_K3", "ou_pis32_ws8_K2", "ou_pis32_ws32_K2"])
+def test_weight_scaled_goldens_both_modes(mode, case):
+    """The reference's own labels for networks with every parameter scaled by 8 and 32
+    (tests/golden/make_golden.py weight_scale), in both GEMM modes: rel-L2 <= 1e-4, through the
+    range guard where the split storage leaves fp16's range."""
+    from golden_util import load
+    from gpu_util import generator, product_equation, product_module, rel_l2_parts
+    f = load(case)
+    eq = product_equation(f)
+    gen = generator(f, eq, product_module(f, eq))
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        y = gen.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu().numpy()
+    parts = rel_l2_parts(y, f["y"])
+    print(case, mode, f"max|y| {np.abs(f['y']).max():.2e}", parts, "fp32 fallback:", gen._fp32_fallback)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts

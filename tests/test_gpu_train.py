@@ -140,3 +140,150 @@ def test_picard_train_saves_reference_label_files(tmp_path):
         assert np.array_equal(tx, seen[i][0]) and np.array_equal(y, seen[i][1])
         batches = list(H5Dataset(p, 256, ["tx", "u_ux"]))
         assert len(batches) == 4 and torch.equal(batches[1][1], torch.from_numpy(seen[i][1][256:512]))
+
+
+HJB = """NAME: {name}
+EQUATION:
+  cls: OUProcessEquation
+  kwargs: {{nx: 100, alpha: 1.0, T: 1.0, num_components: 5, mean_scale: 1.0, var_scale: 2.0, alpha_scale: 4.0}}
+PICARD: {{N: 2}}
+FORCE: true
+DATA:
+  FLOAT: float
+  DATA_SIZE: 256
+  POINTS_PER_CALL: 128
+  SEED: 11
+  kwargs: {{t_always_uniform: true, n_estimate_terminal: 512, n_estimate_integral: 512}}
+TRAIN:
+  N_EPOCHS: 4
+  BATCH_SIZE: 64
+  SUPERVISE_GRADIENT: true
+  LOSS: {{beta: 0.0, SCALER: {{cls: FixedLossScaler, kwargs: {{fixed_weight: 0.1}}}}}}
+  OPTIMIZER: {{kwargs: {{lr: 0.001}}}}
+NETWORK:
+  cls: PicardSolution
+  NEURONS: [512, 512, 512, 512]
+  ACTIVATIONS: ["ELU", "ELU", "ELU", "ELU"]
+  BOUND: None
+  RELOAD: true
+  PISGRADNET: true
+EVAL: {{L2_N_POINTS: 100, TEST_GRAD: true}}
+"""
+
+
+@pytest.mark.parametrize("gemm", ["auto", "f32"])
+def test_picard_train_hjb_pisgradnet_iteration2_labels_vs_oracle(tmp_path, gemm):
+    """`picard train` on the HJB YAML's TRAIN / NETWORK keys (scripts/hjb/base_100d_T1.0_w0.1_0.yaml:
+    PISGradNet 4 x 512, gradient supervision with FixedLossScaler 0.1, TEST_GRAD; the Picard loop of
+    picard_iteration.py:238-299) for 2 iterations, K = 50 on the device path.  Iteration 2's labels
+    come from the TRAINED iterate 1 (not a fresh initialisation): its first two points must match
+    the fp64 oracle on the same counters within rel-L2 1e-4, in the default fp16-split GEMM mode
+    and in exact fp32."""
+    import numpy as np
+
+    from deeppicarditeration_amd import _lib as L
+    from oracle import dpi_oracle as O
+    L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO if gemm == "auto" else L.DPI_GEMM_F32), "gemm")
+    try:
+        f = tmp_path / "hjb.yaml"
+        f.write_text(HJB.format(name=tmp_path / "run"))
+        runner = PicardRunner(load_cfg(str(f)))
+        seen = {}
+        orig = runner.labels
+
+        def labels():  # the iterate the labels are generated from, then the labels
+            u = runner.u_current
+            seen[runner.i] = (type(u).__name__, {k: v.detach().cpu().clone() for k, v in u.state_dict().items()},
+                              *orig())
+            return seen[runner.i][2:]
+
+        runner.labels = labels
+        hist = runner.run()
+        assert [h["iter"] for h in hist] == [1, 2] and all(h["rel_l2_u"] is not None for h in hist)
+        kind, sd1, tx, y = seen[2]
+        assert kind == "PISGradNet" and seen[1][0] == "ZeroSolution"
+        eq = runner.equation
+        oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+        onet = O.PISGradNet({k: v.double().numpy() for k, v in sd1.items()}, oeq, T=1.0)
+        ref = O.labels_grad(oeq, onet, tx[:2].cpu().double().numpy(), 512, 50, 11, 2, 0)
+        got = y[:2].cpu().double().numpy()
+        ev = float(np.linalg.norm(got[:, :1] - ref[:, :1]) / np.linalg.norm(ref[:, :1]))
+        eg = float(np.linalg.norm(got[:, 1:] - ref[:, 1:]) / np.linalg.norm(ref[:, 1:]))
+        print(f"HJB iteration-2 labels ({gemm}): value {ev:.2e} grad {eg:.2e}")
+        assert ev < 1e-4 and eg < 1e-4, (ev, eg)
+    finally:
+        L.check(L.load().dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "gemm")
+
+
+BURGERS_SHIPPED = """NAME: {name}
+EQUATION:
+  cls: Cha
+  kwargs: {{nx: 100, alpha: 1.0, k: 5.0, T: 1.0}}
+PICARD: {{N: 1}}
+FORCE: true
+DATA:
+  FLOAT: float
+  DATA_SIZE: 4096
+  POINTS_PER_CALL: 4096
+  SEED: 5
+  kwargs: {{t_always_uniform: true, n_estimate_terminal: 4096, n_estimate_integral: 4096}}
+TRAIN:
+  N_EPOCHS: 16
+  BATCH_SIZE: 512
+  SUPERVISE_GRADIENT: true
+  LOSS: {{beta: 0.0, SCALER: {{cls: FixedLossScaler, kwargs: {{fixed_weight: 0.0}}}}}}
+NETWORK:
+  NEURONS: [128, 128, 128, 128]
+  ACTIVATIONS: ["ELU", "ELU", "ELU", "ELU"]
+  BOUND: None
+  RELOAD: true
+EVAL: {{L2_N_POINTS: 1000, TEST_GRAD: true}}
+"""
+
+
+def _cha_iteration1_expectation(t, x, k=5.0, T=1.0):
+    """Iteration 1 of Burgers (u = ZeroSolution, so f = fff(., 0, 0) = 0): the label's expectation is
+    E g(X_T) and its x-gradient, X_T = x + sqrt(T - t) xi (zero drift), g = sigmoid(T + k' sum x),
+    k' = k / sqrt(nx) (equations.py:283-305).  sum xi ~ N(0, nx), so both are 1-D Gaussian
+    expectations: Gauss-Hermite with 160 nodes, exact to fp64 rounding."""
+    import numpy as np
+    nx = x.shape[1]
+    kp = k / np.sqrt(nx)
+    z, w = np.polynomial.hermite_e.hermegauss(160)
+    w = w / w.sum()
+    a = T + kp * x.sum(1, keepdims=True) + kp * np.sqrt(nx * (T - t)) * z[None, :]
+    s = 1.0 / (1.0 + np.exp(-a))
+    value = (s * w).sum(1, keepdims=True)
+    grad = kp * (s * (1 - s) * w).sum(1, keepdims=True) * np.ones((1, nx))
+    return np.concatenate([value, grad], 1)
+
+
+def test_picard_train_burgers_shipped_sizes_iteration1_known_answer(tmp_path):
+    """One Burgers Picard iteration at the shipped sizes (scripts/burgers/base_100d_T1.0_w0.0_0.yaml:
+    DATA_SIZE 4096 points x M 4096 paths, K = 50, 100-d, 4 x 128 network, 16 epochs of 512): the
+    4096 x 101 labels against their closed-form expectation (_cha_iteration1_expectation) in units
+    of each label's own Monte-Carlo standard error (from the label moments sum c, sum c^2): the mean
+    squared z-score over all 413,696 entries must be 1 within 5 % and no |z| may exceed 6 — an MC
+    tolerance, not a fixed one.  Then the fit and evaluation run on those labels."""
+    import numpy as np
+    f = tmp_path / "burgers.yaml"
+    f.write_text(BURGERS_SHIPPED.format(name=tmp_path / "run"))
+    runner = PicardRunner(load_cfg(str(f)))
+    runner.i = 1
+    gen = runner.make_generator(runner.u_current)
+    assert gen.K == 50 and gen.n_estimate_integral == 4096
+    tx, y = gen.sample_with_gradients(4096)
+    mom = gen.last_moments.double().cpu().numpy()
+    M = 4096
+    mean, sq = mom[:, 0] / M, mom[:, 1] / M
+    se = np.sqrt(np.maximum(sq - mean ** 2, 0) / M)
+    txh = tx.double().cpu().numpy()
+    exact = _cha_iteration1_expectation(txh[:, :1], txh[:, 1:])
+    z = (y.double().cpu().numpy() - exact) / se
+    mz2 = float((z ** 2).mean())
+    print(f"Burgers iteration 1, 4096 x 4096 x K=50: mean z^2 {mz2:.4f}, max |z| {np.abs(z).max():.2f}, "
+          f"value rel-L2 vs E[label] {np.linalg.norm(y.cpu().numpy()[:, 0] - exact[:, 0]) / np.linalg.norm(exact[:, 0]):.2e}")
+    assert 0.95 < mz2 < 1.05 and np.abs(z).max() < 6.0
+    runner.i = 0
+    hist = runner.run()
+    assert len(hist) == 1 and hist[0]["labels"] == 4096 and hist[0]["path_labels_per_s"] > 1e7
