@@ -1,0 +1,159 @@
+// A/B microbenchmark: the product 128 x 128 split GEMM (dpi_gemm.h k_gemm_x3h: W and X tiles both
+// through a 2-slot LDS-DMA ring, one chunk of look-ahead) against k_gemm_x3g (W alone through a
+// deeper LDS-DMA ring, each wave's X fragments loaded from global straight into registers XD chunks
+// ahead).  Same products per output in the same order, so the outputs must be bitwise equal; the
+// harness counts differing words.  Shapes: the HJB chain's 262,144 x 512 x 512 (ELU, DELU), a
+// partial last m-tile, K = 128 / 96 (short and odd chunk counts) and K = 1,024 from two sources.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -o tools/ubench_x3g tools/ubench_x3g.hip
+//   tools/ubench_x3g [M] [iters]
+// Result (r03f, profiles/r03f_ubench_x3g.txt): bitwise equal, but 763-779 us (ELU) / 809 us (DELU)
+// against x3h's 543-554 / 593 us.  A fragment load touches 16 rows x 4 half-lines (16 cache lines
+// per wave-instruction, twice the LDS-DMA's 8) and the two waves sharing an m-range load the same
+// bytes: 4x the L1 line accesses of the DMA for X, which the vector L1 does not sustain.  XD = 2
+// needs > 256 VGPRs; its spills copy inline-asm load destinations before the counted wait (wrong
+// results) and faulted the GPU once — removed, with a static_assert against it.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../deeppicarditeration_amd/csrc/dpi_device.h"
+#include "x3g_proto.h"
+
+using namespace dpi;
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e_ = (x);                                                         \
+    if (e_ != hipSuccess) {                                                      \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                              \
+    }                                                                            \
+  } while (0)
+
+__global__ void k_fill(float* rows, int M, int Kp, int ld, uint32_t seed, float scale) {
+  const int m = blockIdx.x, tid = threadIdx.x;
+  if (m >= M) return;
+  for (int idx = tid; idx < (Kp / 32) * 4; idx += blockDim.x) {
+    const int u = idx >> 2, q = idx & 3;
+    float v[8];
+    for (int j = 0; j < 8; ++j) {
+      uint32_t h = (uint32_t)m * 2654435761u ^ (uint32_t)(idx * 8 + j) * 2246822519u ^ seed;
+      h ^= h >> 15;
+      h *= 2654435761u;
+      h ^= h >> 13;
+      v[j] = scale * ((float)(h >> 8) * (1.0f / 8388608.0f) - 1.0f);
+    }
+    x3_put8(rows + (size_t)m * ld, 0, u, q, v);
+  }
+}
+
+struct Case {
+  int M, Kp, Np, nk1;  // K = Kp: chunks < nk1 from X (row stride ldx), the rest from X2
+  int ldx, ldx2;
+};
+
+struct Bufs {
+  uint32_t* W;
+  float *X, *X2, *AUX, *OUT, *REF, *bias;
+};
+
+// kind 0: k_gemm_x3h, 1: x3g XD = 1
+template <int EPI>
+static void launch(int kind, const Case& c, const Bufs& b, float* out) {
+  const int nnt = c.Np / 128, nmt = (c.M + 127) / 128;
+  const float* bias = EPI == EPI_DELU ? nullptr : b.bias;
+  if (kind == 0)
+    hipLaunchKernelGGL(k_gemm_x3h<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.Np);
+  else
+    hipLaunchKernelGGL((k_gemm_x3g<EPI, 1>), dim3(nnt * nmt), dim3(X3G_THREADS), 0, 0, c.M, c.Kp, nnt, b.W,
+                       1.0f / 16.0f, b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.Np);
+}
+
+template <int EPI>
+static double timed(int kind, const Case& c, const Bufs& b, int iters) {
+  launch<EPI>(kind, c, b, b.OUT);
+  CK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) launch<EPI>(kind, c, b, b.OUT);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  return ms * 1e3 / iters;
+}
+
+static size_t differing(const Case& c, const Bufs& b) {
+  std::vector<uint32_t> a((size_t)c.M * c.Np), r((size_t)c.M * c.Np);
+  CK(hipMemcpy(a.data(), b.OUT, a.size() * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(r.data(), b.REF, r.size() * 4, hipMemcpyDeviceToHost));
+  size_t bad = 0;
+  for (size_t i = 0; i < a.size(); ++i) bad += a[i] != r[i];
+  return bad;
+}
+
+template <int EPI>
+static void compare(const char* name, const Case& c, const Bufs& b, int iters, int reps) {
+  CK(hipMemset(b.REF, 0, (size_t)c.M * c.Np * 4));
+  launch<EPI>(0, c, b, b.REF);
+  CK(hipDeviceSynchronize());
+  for (int rep = 0; rep < reps; ++rep)
+    for (int kind = 0; kind < 2; ++kind) {
+      CK(hipMemset(b.OUT, 0xFF, (size_t)c.M * c.Np * 4));
+      const double us = timed<EPI>(kind, c, b, iters);
+      const size_t bad = differing(c, b);
+      std::printf("%-5s %-34s %-10s %8.1f us  %6.1f TF/s(split-eff)  differing words %zu\n",
+                  EPI == EPI_DELU ? "delu" : "elu", name, kind == 0 ? "x3h" : "x3g XD=1", us,
+                  2.0 * c.M * (double)c.Kp * c.Np / (us * 1e-6) / 1e12, bad);
+      std::fflush(stdout);
+    }
+}
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? std::atoi(argv[1]) : 262144;
+  const int iters = argc > 2 ? std::atoi(argv[2]) : 20;
+  const int KMAX = 1024, NP = 512;
+  Bufs b;
+  CK(hipMalloc(&b.W, (size_t)NP * KMAX * 4));
+  CK(hipMalloc(&b.X, (size_t)M * 512 * 4));
+  CK(hipMalloc(&b.X2, (size_t)M * 512 * 4));
+  CK(hipMalloc(&b.AUX, (size_t)M * NP * 4));
+  CK(hipMalloc(&b.OUT, (size_t)M * NP * 4));
+  CK(hipMalloc(&b.REF, (size_t)M * NP * 4));
+  CK(hipMalloc(&b.bias, NP * 4));
+  hipLaunchKernelGGL(k_fill, dim3(NP), dim3(128), 0, 0, reinterpret_cast<float*>(b.W), NP, KMAX, KMAX, 7u, 0.8f);
+  hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, b.X, M, 512, 512, 11u, 1.0f);
+  hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, b.X2, M, 512, 512, 17u, 1.0f);
+  hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, b.AUX, M, NP, NP, 13u, 1.5f);
+  std::vector<float> hb(NP);
+  for (int i = 0; i < NP; ++i) hb[i] = 0.01f * (float)((i * 37) % 17 - 8);
+  CK(hipMemcpy(b.bias, hb.data(), NP * 4, hipMemcpyHostToDevice));
+  CK(hipDeviceSynchronize());
+
+  // the W image is (NP x KMAX); a case with Kp < KMAX reads its first Kp words per row as a
+  // (NP x Kp) matrix, which is what the kernels take (row stride Kp)
+  const Case full{M, 512, NP, 16, 512, 512};
+  compare<EPI_BIAS_ELU>("262144x512x512", full, b, iters, 3);
+  compare<EPI_DELU>("262144x512x512", full, b, iters, 3);
+  const Case part{M - 64, 512, NP, 16, 512, 512};
+  compare<EPI_BIAS_ELU>("partial m-tile (M - 64)", part, b, iters, 1);
+  const Case k128{M, 128, NP, 4, 512, 512};
+  compare<EPI_BIAS_ELU>("K 128", k128, b, iters, 1);
+  compare<EPI_DELU>("K 128", k128, b, iters, 1);
+  const Case k96{M - 192, 96, NP, 3, 512, 512};
+  compare<EPI_BIAS_ELU>("K 96, M - 192", k96, b, iters, 1);
+  const Case k1024{M, 1024, NP, 16, 512, 512};
+  compare<EPI_BIAS_ELU>("K 1024 two-source", k1024, b, iters, 1);
+  const Case k32{M, 32, NP, 1, 512, 512};
+  compare<EPI_BIAS_ELU>("K 32 (one chunk)", k32, b, iters, 1);
+  return 0;
+}
