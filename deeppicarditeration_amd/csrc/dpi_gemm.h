@@ -528,25 +528,50 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3h(int M, int Kp, int 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
   const int il = lane & 15, ql = lane >> 4;
   const int nk = Kp >> 5;
-  const uint32_t* Xw = reinterpret_cast<const uint32_t*>(X);
-  const uint32_t* X2w = reinterpret_cast<const uint32_t*>(X2);
+  // LDS-DMA in buffer form (r03f): the wave id made provably uniform, so each DMA's LDS destination
+  // is scalar (m0 from SALU alone), and each lane's row offset fixed in a VGPR with the chunk's
+  // column offset in soffset — no per-DMA VALU address arithmetic or readfirstlane.  Bitwise equal;
+  // 567-573 -> 528-536 us (ELU), 600-609 -> 579-592 us (DELU) at 262,144 x 512 x 512
+  // (profiles/r03f_ubench_x3hb.txt).  The resources start at the block's own tiles (W rows n0..,
+  // X rows m0..), so the 32-bit offsets stay small whatever the row stride of the activation
+  // workspace (thousands of words: the whole chain's row) or M.
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int mrows = min(BM, M - m0);  // >= 1: the grid holds only tiles with rows
+  auto tile_rsrc = [](const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rw = tile_rsrc(W + (size_t)n0 * Kp, (size_t)BN * Kp * 4);
+  const __amdgpu_buffer_rsrc_t rx = tile_rsrc(X + (size_t)m0 * ldx, (size_t)mrows * ldx * 4);
+  const __amdgpu_buffer_rsrc_t rx2 = tile_rsrc(X2 + (size_t)m0 * ldx2, (size_t)mrows * ldx2 * 4);
+  // wave-instruction k fills rows 8w..8w+7, w = 4k + wave: k < 4 the W tile, k >= 4 the X tile
+  int vw[PER_WAVE / 2], vx[PER_WAVE / 2], vx2[PER_WAVE / 2];
+#pragma unroll
+  for (int k = 0; k < PER_WAVE; ++k) {
+    const int w = k * NWAVE + wv;
+    const int r = 8 * w + (lane >> 3);
+    const int g = (lane & 7) ^ x3_swz(r);
+    if (k < PER_WAVE / 2) {
+      vw[k] = r * Kp * 4 + 16 * g;
+    } else {
+      const int xr = min(r - BN, mrows - 1);  // rows past M load the last row
+      vx[k - PER_WAVE / 2] = xr * ldx * 4 + 16 * g;
+      vx2[k - PER_WAVE / 2] = xr * ldx2 * 4 + 16 * g;
+    }
+  }
   auto issue = [&](int c, int slot) {
     uint32_t* dst = sm + slot * STAGE;
     const bool one = c < nk1;  // two-source K as in x3_tile
-    const uint32_t* xb = one ? Xw + 32 * c : X2w + 32 * (c - nk1);
-    const int ld = one ? ldx : ldx2;
+    const int sx = one ? 128 * c : 128 * (c - nk1);
 #pragma unroll
     for (int k = 0; k < PER_WAVE; ++k) {
-      const int w = k * NWAVE + wv;
-      const int r = 8 * w + (lane >> 3);
-      const int g = (lane & 7) ^ x3_swz(r);
-      const uint32_t* src;
-      if (r < BN)
-        src = W + (size_t)(n0 + r) * Kp + 32 * c + 4 * g;
+      __attribute__((address_space(3))) void* d =
+          (__attribute__((address_space(3))) void*)(dst + 256 * (k * NWAVE + wvu));
+      if (k < PER_WAVE / 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, d, 16, vw[k], 128 * c, 0, 0);
+      else if (one)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx[k - PER_WAVE / 2], sx, 0, 0);
       else
-        src = xb + (size_t)min(m0 + r - BN, M - 1) * ld + 4 * g;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx2, d, 16, vx2[k - PER_WAVE / 2], sx, 0, 0);
     }
   };
   auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {

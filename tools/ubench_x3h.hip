@@ -1,17 +1,22 @@
-// A/B microbenchmark: the product 128 x 128 split GEMM (dpi_gemm.h k_gemm_x3h: W and X tiles both
-// through a 2-slot LDS-DMA ring, one chunk of look-ahead) against k_gemm_x3g (W alone through a
-// deeper LDS-DMA ring, each wave's X fragments loaded from global straight into registers XD chunks
-// ahead).  Same products per output in the same order, so the outputs must be bitwise equal; the
-// harness counts differing words.  Shapes: the HJB chain's 262,144 x 512 x 512 (ELU, DELU), a
-// partial last m-tile, K = 128 / 96 (short and odd chunk counts) and K = 1,024 from two sources.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -o tools/ubench_x3g tools/ubench_x3g.hip
-//   tools/ubench_x3g [M] [iters]
-// Result (r03f, profiles/r03f_ubench_x3g.txt): bitwise equal, but 763-779 us (ELU) / 809 us (DELU)
-// against x3h's 543-554 / 593 us.  A fragment load touches 16 rows x 4 half-lines (16 cache lines
-// per wave-instruction, twice the LDS-DMA's 8) and the two waves sharing an m-range load the same
-// bytes: 4x the L1 line accesses of the DMA for X, which the vector L1 does not sustain.  XD = 2
-// needs > 256 VGPRs; its spills copy inline-asm load destinations before the counted wait (wrong
-// results) and faulted the GPU once — removed, with a static_assert against it.
+// A/B microbenchmark of the 512-wide split GEMMs: k_gemm_x3h (128 x 128 tile, two blocks per CU,
+// buffer-form LDS-DMA since r03f) against k_gemm_x3 (256 x 128, pointer-form LDS-DMA), whose
+// products per output run in the same order, so the outputs must be bitwise equal; the harness
+// counts differing words.  Shapes: the HJB chain's 262,144 x 512 x 512 (ELU, DELU), a partial last
+// m-tile, K = 128 / 96 (short and odd chunk counts), K = 1,024 from two sources, one chunk, and a
+// 2,304-word row stride (the activation workspace's: row offsets past 2^31 bytes).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -o tools/ubench_x3h tools/ubench_x3h.hip
+//   tools/ubench_x3h [M] [iters]
+//
+// Record (r03f, profiles/r03f_ubench_x3g.txt, r03f_ubench_x3hb.txt):
+//  - buffer-form DMA in k_gemm_x3h (scalar LDS destinations: the wave id through readfirstlane;
+//    fixed per-lane row offsets, the chunk's column in soffset): bitwise equal, ELU 567-573 ->
+//    528-536 us, DELU 600-609 -> 579-592 us, K 128 261 -> 250 / 320 -> 307 us;
+//  - k_gemm_x3g, X fragments loaded from global straight into registers (W alone through a deeper
+//    LDS-DMA ring): bitwise equal but 763-793 us (ELU) / 809-834 us (DELU).  A fragment load
+//    touches 16 rows x 4 half-lines per wave-instruction (the DMA: 8 rows x 1 line) and both waves
+//    of an m-range load the same bytes — 4x the vector-L1 line accesses for X.  Its inline-asm
+//    loads (the compiler's own waits fell to vmcnt(0) with VGPR loads and LDS-DMA both in flight)
+//    faulted the GPU twice (XD = 2 spilling, then K = 96 with a partial m-tile): removed.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,7 +26,6 @@
 #include <vector>
 
 #include "../deeppicarditeration_amd/csrc/dpi_device.h"
-#include "x3g_proto.h"
 
 using namespace dpi;
 
@@ -54,6 +58,7 @@ __global__ void k_fill(float* rows, int M, int Kp, int ld, uint32_t seed, float 
 struct Case {
   int M, Kp, Np, nk1;  // K = Kp: chunks < nk1 from X (row stride ldx), the rest from X2
   int ldx, ldx2;
+  int ldaux = 512;  // AUX rows (DELU operand), Np = 512 words unless the workspace's stride
 };
 
 struct Bufs {
@@ -61,17 +66,21 @@ struct Bufs {
   float *X, *X2, *AUX, *OUT, *REF, *bias;
 };
 
-// kind 0: k_gemm_x3h, 1: x3g XD = 1
+// kind 0: k_gemm_x3 (256 x 128 tile, pointer-form LDS-DMA: the reference for bitwise equality),
+// 1: k_gemm_x3h (128 x 128, two blocks per CU, buffer-form LDS-DMA since r03f)
 template <int EPI>
 static void launch(int kind, const Case& c, const Bufs& b, float* out) {
-  const int nnt = c.Np / 128, nmt = (c.M + 127) / 128;
   const float* bias = EPI == EPI_DELU ? nullptr : b.bias;
-  if (kind == 0)
+  const int nnt = c.Np / 128;
+  if (kind == 0) {
+    const int nmt = (c.M + X3_BM - 1) / X3_BM;
+    hipLaunchKernelGGL((k_gemm_x3<EPI, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux, 0);
+  } else {
+    const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
     hipLaunchKernelGGL(k_gemm_x3h<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
-                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.Np);
-  else
-    hipLaunchKernelGGL((k_gemm_x3g<EPI, 1>), dim3(nnt * nmt), dim3(X3G_THREADS), 0, 0, c.M, c.Kp, nnt, b.W,
-                       1.0f / 16.0f, b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.Np);
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
+  }
 }
 
 template <int EPI>
@@ -112,7 +121,7 @@ static void compare(const char* name, const Case& c, const Bufs& b, int iters, i
       const double us = timed<EPI>(kind, c, b, iters);
       const size_t bad = differing(c, b);
       std::printf("%-5s %-34s %-10s %8.1f us  %6.1f TF/s(split-eff)  differing words %zu\n",
-                  EPI == EPI_DELU ? "delu" : "elu", name, kind == 0 ? "x3h" : "x3g XD=1", us,
+                  EPI == EPI_DELU ? "delu" : "elu", name, kind == 0 ? "x3 (256)" : "x3h", us,
                   2.0 * c.M * (double)c.Kp * c.Np / (us * 1e-6) / 1e12, bad);
       std::fflush(stdout);
     }
@@ -155,5 +164,19 @@ int main(int argc, char** argv) {
   compare<EPI_BIAS_ELU>("K 1024 two-source", k1024, b, iters, 1);
   const Case k32{M, 32, NP, 1, 512, 512};
   compare<EPI_BIAS_ELU>("K 32 (one chunk)", k32, b, iters, 1);
+  // the activation workspace's row stride: X and AUX rows 2,304 words apart (M x 2,304 x 4 B > 2 GiB)
+  const int LDW = 2304;
+  float* Xw;
+  CK(hipMalloc(&Xw, (size_t)M * LDW * 4));
+  hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, Xw + 1024, M, 512, LDW, 19u, 1.0f);
+  hipLaunchKernelGGL(k_fill, dim3(M), dim3(128), 0, 0, Xw + 1536, M, 512, LDW, 23u, 1.5f);
+  Bufs bw = b;
+  bw.X = Xw + 1024;
+  bw.X2 = Xw + 1024;
+  bw.AUX = Xw + 1536;
+  const Case wide{M - 64, 512, NP, 16, LDW, LDW, LDW};
+  compare<EPI_BIAS_ELU>("row stride 2304, M - 64", wide, bw, iters, 1);
+  compare<EPI_DELU>("row stride 2304, M - 64", wide, bw, iters, 1);
+  CK(hipFree(Xw));
   return 0;
 }
