@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../deeppicarditeration_amd/csrc/dpi_device.h"
+#include "x3q_proto.h"
 
 using namespace dpi;
 
@@ -67,7 +68,8 @@ struct Bufs {
 };
 
 // kind 0: k_gemm_x3 (256 x 128 tile, pointer-form LDS-DMA: the reference for bitwise equality),
-// 1: k_gemm_x3h (128 x 128, two blocks per CU, buffer-form LDS-DMA since r03f)
+// 1: k_gemm_x3h (128 x 128, two blocks per CU, buffer-form LDS-DMA since r03f), 2: k_gemm_x3q
+// (tools/x3q_proto.h: x3h with a 3-slot X ring, X two chunks ahead)
 template <int EPI>
 static void launch(int kind, const Case& c, const Bufs& b, float* out) {
   const float* bias = EPI == EPI_DELU ? nullptr : b.bias;
@@ -76,9 +78,17 @@ static void launch(int kind, const Case& c, const Bufs& b, float* out) {
     const int nmt = (c.M + X3_BM - 1) / X3_BM;
     hipLaunchKernelGGL((k_gemm_x3<EPI, 4>), dim3(nnt * nmt), dim3(X3_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
                        b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux, 0);
-  } else {
+  } else if (kind == 1) {
     const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
     hipLaunchKernelGGL(k_gemm_x3h<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
+  } else if (kind == 3) {
+    const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
+    hipLaunchKernelGGL(k_gemm_x3e<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
+  } else {
+    const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
+    hipLaunchKernelGGL(k_gemm_x3q<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
                        b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
   }
 }
@@ -116,12 +126,12 @@ static void compare(const char* name, const Case& c, const Bufs& b, int iters, i
   launch<EPI>(0, c, b, b.REF);
   CK(hipDeviceSynchronize());
   for (int rep = 0; rep < reps; ++rep)
-    for (int kind = 0; kind < 2; ++kind) {
+    for (int kind : {0, 1, 3}) {
       CK(hipMemset(b.OUT, 0xFF, (size_t)c.M * c.Np * 4));
       const double us = timed<EPI>(kind, c, b, iters);
       const size_t bad = differing(c, b);
       std::printf("%-5s %-34s %-10s %8.1f us  %6.1f TF/s(split-eff)  differing words %zu\n",
-                  EPI == EPI_DELU ? "delu" : "elu", name, kind == 0 ? "x3 (256)" : "x3h", us,
+                  EPI == EPI_DELU ? "delu" : "elu", name, kind == 0 ? "x3 (256)" : kind == 1 ? "x3h" : kind == 2 ? "x3q" : "x3e", us,
                   2.0 * c.M * (double)c.Kp * c.Np / (us * 1e-6) / 1e12, bad);
       std::fflush(stdout);
     }
@@ -150,6 +160,57 @@ int main(int argc, char** argv) {
 
   // the W image is (NP x KMAX); a case with Kp < KMAX reads its first Kp words per row as a
   // (NP x Kp) matrix, which is what the kernels take (row stride Kp)
+  if (argc > 3 && std::strcmp(argv[3], "stamp") == 0) {  // per-wave s_memtime stamps of k_gemm_x3hs
+    const int nmt = (M + X3H_BM - 1) / X3H_BM, nnt = NP / 128, nb = nmt * nnt;
+    unsigned long long* st;
+    CK(hipMalloc(&st, (size_t)nb * 4 * 8 * 8));
+    for (int e = 0; e < 2; ++e) {
+      CK(hipMemset(st, 0, (size_t)nb * 4 * 8 * 8));
+      for (int rep = 0; rep < 30; ++rep) {
+        if (e == 0)
+          hipLaunchKernelGGL(k_gemm_x3hs<EPI_BIAS_ELU>, dim3(nb), dim3(X3H_THREADS), 0, 0, st, M, 512, nnt, b.W,
+                             1.0f / 16.0f, b.X, 512, b.X, 512, 16, b.OUT, NP, b.bias, b.AUX, NP);
+        else
+          hipLaunchKernelGGL(k_gemm_x3hs<EPI_DELU>, dim3(nb), dim3(X3H_THREADS), 0, 0, st, M, 512, nnt, b.W,
+                             1.0f / 16.0f, b.X, 512, b.X, 512, 16, b.OUT, NP, nullptr, b.AUX, NP);
+      }
+      CK(hipDeviceSynchronize());
+      std::vector<unsigned long long> h((size_t)nb * 4 * 8);
+      CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long tmin = ~0ull, tmax = 0;
+      double pro = 0, loop = 0, epi = 0, wait = 0, vm = 0, rt = 0, cyc = 0;
+      size_t nw = 0;
+      for (size_t w = 0; w < (size_t)nb * 4; ++w) {
+        const unsigned long long* o = &h[w * 8];
+        if (!o[0]) continue;
+        ++nw;
+        tmin = std::min(tmin, o[0]);
+        tmax = std::max(tmax, o[3]);
+        pro += o[1] - o[0];
+        loop += o[2] - o[1];
+        epi += o[3] - o[2];
+        wait += o[4];
+        vm += o[5];
+        rt += o[7];
+        cyc += o[3] - o[0];
+      }
+      std::printf("in-kernel clock %.3f GHz (s_memtime / s_memrealtime at 100 MHz, mean over waves)\n",
+                  cyc / rt * 0.1);
+      std::printf("%s: %zu live waves; launch span %.0f cycles; per wave: prologue %.0f, main loop %.0f (of it "
+                  "wait+barrier %.0f, vmcnt %.0f), epilogue %.0f cycles; MFMA issue per wave 12288 cycles\n",
+                  e == 0 ? "elu" : "delu", nw, (double)(tmax - tmin), pro / nw, loop / nw, wait / nw, vm / nw,
+                  epi / nw);
+      // block lifetimes in order of start on one CU: the first 6 blocks' (start, end) relative to launch start
+      std::printf("  first blocks (start, after prologue, after loop, end) - launch start:\n");
+      for (int blk = 0; blk < 6; ++blk) {
+        const unsigned long long* o = &h[(size_t)blk * 4 * 8];
+        std::printf("   block %d hwid %08llx: %llu %llu %llu %llu\n", blk, o[6], o[0] - tmin, o[1] - tmin, o[2] - tmin,
+                    o[3] - tmin);
+      }
+      std::fflush(stdout);
+    }
+    return 0;
+  }
   const Case full{M, 512, NP, 16, 512, 512};
   compare<EPI_BIAS_ELU>("262144x512x512", full, b, iters, 3);
   compare<EPI_DELU>("262144x512x512", full, b, iters, 3);
