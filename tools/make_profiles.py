@@ -46,10 +46,13 @@ for wl, anchor in ANCHOR.items():
             indent=1))
     if len(pmc) < 2:
         continue
-    calls = sum(v["dispatches"] for k, v in pmc["FETCH_SIZE"].items() if k.startswith(anchor))
-    fe = sum(v["total_kb"] for v in pmc["FETCH_SIZE"].values()) / calls
-    wr = sum(v["total_kb"] for v in pmc["WRITE_SIZE"].values()) / calls
-    t = {"workload": wl, "anchor_kernel": anchor, "calls": calls, "FETCH_SIZE_KB_per_call": fe,
+    # each pass is its own bench run (the prewarm is timed, so the passes hold different numbers of
+    # calls): every counter's total is divided by the anchor launches of its own pass
+    ncalls = {c: sum(v["dispatches"] for k, v in pmc[c].items() if k.startswith(anchor)) for c in pmc}
+    calls = ncalls["FETCH_SIZE"]
+    fe = sum(v["total_kb"] for v in pmc["FETCH_SIZE"].values()) / ncalls["FETCH_SIZE"]
+    wr = sum(v["total_kb"] for v in pmc["WRITE_SIZE"].values()) / ncalls["WRITE_SIZE"]
+    t = {"workload": wl, "anchor_kernel": anchor, "calls": calls, "calls_write_pass": ncalls["WRITE_SIZE"], "FETCH_SIZE_KB_per_call": fe,
          "WRITE_SIZE_KB_per_call": wr, "hbm_bytes_per_launch": (2 * fe + wr) * 1024,
          "note": "separate --pmc passes; FETCH_SIZE doubled per the gfx950 correction (an upper bound for the "
                  "non-16-B loads); Infinity-Cache hits are counted by these fabric-side counters; all kernels of "
