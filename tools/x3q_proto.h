@@ -629,3 +629,203 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3e(int M, int Kp, int 
 }
 
 }  // namespace dpi
+
+namespace dpi {
+// k_gemm_x3t: k_gemm_x3h on v_mfma_f32_32x32x16_f16 — twice the MACs per instruction at the same 8
+// cycles of held issue, so the partner wave's VALU / DMA / ds_read issue gets 3 of every 4 cycles
+// instead of 1 of 2.  Same 128 x 128 tile, 4 waves of 64 x 64 (2 x 2 tiles of 32 x 32), same
+// buffer-form LDS-DMA ring; the LDS image is swizzled for this kernel's fragment reads (lane l reads
+// row l % 32, granule pair 2 s + l / 32 for k-step s): granule g of row r sits at g ^ ((r >> 1) & 7),
+// which gives each ds_read_b128 lane group 16 distinct (row parity, 16-B slot) pairs.  Output lane l,
+// register r of tile (N, Mt): path m = 32 Mt + l % 32, unit 32 N + 8 (r / 4) + 4 (l / 32) + r % 4 —
+// granule pairs q = l / 32 (r = 0-3, 8-11) and q = 2 + l / 32 (r = 4-7, 12-15) of one row, whole.
+// Not bitwise equal to the 16x16x32 chain (16-deep partial products).
+__device__ __forceinline__ int x3t_swz(int r) { return (r >> 1) & 7; }
+
+template <int EPI>
+__global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3t(int M, int Kp, int n_ntiles, const uint32_t* __restrict__ W,
+                                                             float wscale, const float* __restrict__ X, int ldx,
+                                                             const float* __restrict__ X2, int ldx2, int nk1,
+                                                             float* __restrict__ OUT, int ldc,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ AUX, int ldaux) {
+  constexpr int BN = 128, BM = X3H_BM, STAGE = X3HLds::STAGE, NWAVE = X3H_THREADS / 64;
+  constexpr int PER_WAVE = (BN + BM) / 8 / NWAVE;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f16v __attribute__((ext_vector_type(16)));
+  __shared__ X3HLds lds;
+  uint32_t* sm = lds.sm;
+  const int tile = x3_tile_of_block(), mt = tile / n_ntiles, ntl = tile - mt * n_ntiles;
+  const int m0 = mt * BM, n0 = ntl * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int i32 = lane & 31, g2 = lane >> 5;
+  const int nk = Kp >> 5;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int mrows = min(BM, M - m0);
+  auto tile_rsrc = [](const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rw = tile_rsrc(W + (size_t)n0 * Kp, (size_t)BN * Kp * 4);
+  const __amdgpu_buffer_rsrc_t rx = tile_rsrc(X + (size_t)m0 * ldx, (size_t)mrows * ldx * 4);
+  const __amdgpu_buffer_rsrc_t rx2 = tile_rsrc(X2 + (size_t)m0 * ldx2, (size_t)mrows * ldx2 * 4);
+  int vw[PER_WAVE / 2], vx[PER_WAVE / 2], vx2[PER_WAVE / 2];
+#pragma unroll
+  for (int k = 0; k < PER_WAVE; ++k) {
+    const int w = k * NWAVE + wv;
+    const int r = 8 * w + (lane >> 3);
+    const int g = (lane & 7) ^ x3t_swz(r);
+    if (k < PER_WAVE / 2) {
+      vw[k] = r * Kp * 4 + 16 * g;
+    } else {
+      const int xr = min(r - BN, mrows - 1);
+      vx[k - PER_WAVE / 2] = xr * ldx * 4 + 16 * g;
+      vx2[k - PER_WAVE / 2] = xr * ldx2 * 4 + 16 * g;
+    }
+  }
+  auto issue = [&](int c, int slot) {
+    uint32_t* dst = sm + slot * STAGE;
+    const bool one = c < nk1;
+    const int sx = one ? 128 * c : 128 * (c - nk1);
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+      __attribute__((address_space(3))) void* d =
+          (__attribute__((address_space(3))) void*)(dst + 256 * (k * NWAVE + wvu));
+      if (k < PER_WAVE / 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, d, 16, vw[k], 128 * c, 0, 0);
+      else if (one)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, d, 16, vx[k - PER_WAVE / 2], sx, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx2, d, 16, vx2[k - PER_WAVE / 2], sx, 0, 0);
+    }
+  };
+  // fragment of LDS row `row`, k-step s: granule pair q = 2 s + l / 32 (hi granule 2q, lo 2q + 1)
+  auto frag = [&](const uint32_t* buf, int row, int s, h8& h, h8& l) {
+    const int sw = x3t_swz(row), q = 2 * s + g2;
+    const uint32_t* rp = buf + row * 32;
+    h = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * q) ^ sw)));
+    l = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * q + 1) ^ sw)));
+  };
+  f16v acc[2][2];  // [N][Mt]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  h8 ah[2][2][2], al[2][2][2], bh[2][2][2], bl[2][2][2];  // [set][tile][k-step]
+  auto load = [&](int slot, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    const uint32_t* buf = sm + slot * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) frag(buf, wn * 64 + 32 * t + i32, s, ah[F][t][s], al[F][t][s]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) frag(buf, BN + wm * 64 + 32 * t + i32, s, bh[F][t][s], bl[F][t][s]);
+    }
+  };
+  auto mma = [&](auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[F][a][s], bh[F][b][s], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[F][a][s], bl[F][b][s], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[F][a][s], bh[F][b][s], acc[a][b], 0, 0, 0);
+        }
+  };
+  auto body = [&](int u, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < nk) issue(u + 2, u & 1);
+    load((u + 1) & 1, std::integral_constant<int, F ^ 1>{});
+    mma(Fc);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // 16 ds_reads among 24 MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    }
+  };
+  const bool has_bias = (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && bias != nullptr;
+  float* sbias = reinterpret_cast<float*>(sm + 2 * STAGE);
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (has_bias && tid < BN / 4) bv = *reinterpret_cast<const float4*>(bias + n0 + 4 * tid);
+  __builtin_amdgcn_s_setprio(2);
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (has_bias && tid < BN / 4) *reinterpret_cast<float4*>(sbias + 4 * tid) = bv;
+  __builtin_amdgcn_s_barrier();
+  if (m0 + wm * 64 >= M) {
+    for (int u = 0; u + 1 < nk; ++u) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (u + 2 < nk) issue(u + 2, u & 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+  load(0, std::integral_constant<int, 0>{});
+  int u = 0;
+  for (; u + 2 < nk; u += 2) {
+    body(u, std::integral_constant<int, 0>{});
+    body(u + 1, std::integral_constant<int, 1>{});
+  }
+  if (u + 1 < nk) {
+    body(u, std::integral_constant<int, 0>{});
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mma(std::integral_constant<int, 1>{});
+  } else {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    mma(std::integral_constant<int, 0>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // epilogue: tile (a, b) lane l holds OUT[m0 + 64 wm + 32 b + l % 32][n0 + 64 wn + 32 a + col(r)]
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int m = m0 + wm * 64 + 32 * b + i32;
+    if (m >= M) continue;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int U = (n0 >> 5) + wn * 2 + a;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // granule pair q = 2 h + l / 32: registers 4h..4h+3 and 8+4h..8+4h+3
+        const int q = 2 * h + g2;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[a][b][4 * h + r] * wscale;
+          v[4 + r] = acc[a][b][8 + 4 * h + r] * wscale;
+        }
+        if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
+          if (has_bias) {
+            const float* bsrc = sbias + 32 * (wn * 2 + a) + 4 * q;
+            const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+            const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
+            v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+            v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+          }
+          if (EPI == EPI_BIAS_ELU)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+        } else {
+          float av[8];
+          x3_get8(AUX + (size_t)m * ldaux, 0, U, q, av);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= av[j] > 0.f ? 1.0f : av[j] + 1.0f;
+        }
+        x3_put8(OUT + (size_t)m * ldc, 0, U, q, v);
+      }
+    }
+  }
+}
+}  // namespace dpi
