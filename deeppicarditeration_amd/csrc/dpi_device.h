@@ -905,8 +905,16 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
   // tangent sweep over the state dimensions.  The lam z^2 terms accumulate in register pairs
   // (v_pk_mul_f32 + v_pk_fma_f32: one VALU issue per unit instead of two).
   float s1 = 0.f, s2 = 0.f;
-  for (int d = 0; d < e.nx; ++d) {
-    float z[HT][4];
+  // z_0 = W1x[:, d] of the next direction is read from LDS while this direction's MFMAs run: two
+  // register sets, the direction loop unrolled by 2 so they swap roles without copies
+  auto ldz = [&](int d, float (&zz)[HT][4]) {
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zz[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+  };
+  // one direction: z (in) is clobbered; zn receives z_0 of direction dn
+  auto direction = [&](int d, float (&z)[HT][4], float (&zn)[HT][4], int dn) {
     f32x2 term2 = {0.f, 0.f};
     auto acc_terms = [&](const float (&lm)[HT][4], const float (&zz)[HT][4]) {
 #pragma unroll
@@ -917,10 +925,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
           term2 = (l2 * z2) * z2 + term2;
         }
     };
-#pragma unroll
-    for (int T = 0; T < HT; ++T)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
+    ldz(dn, zn);
     acc_terms(lam[0], z);
 #pragma unroll
     for (int l = 1; l < L; ++l) {
@@ -938,7 +943,15 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     const float c = (float)sh.cnt[d * P + pp];
     s1 = fmaf(c, ud, s1);
     s2 = fmaf(c, fabsf(ud), s2);
+  };
+  float za[HT][4], zb[HT][4];
+  ldz(0, za);
+  int d = 0;
+  for (; d + 1 < e.nx; d += 2) {
+    direction(d, za, zb, d + 1);
+    direction(d + 1, zb, za, d + 2 < e.nx ? d + 2 : d + 1);
   }
+  if (d < e.nx) direction(d, za, zb, d);
   s1_out = s1;
   s2_out = s2;
 }
