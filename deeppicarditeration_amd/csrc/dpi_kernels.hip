@@ -1122,6 +1122,19 @@ static int pis_rollout_unroll() {
   return v;
 }
 
+// Rollout blocks per CU in each prepare-stream grid (DPI_PIS_PREP_PER_CU, default 3).  One block per
+// CU left the next batch's rollout (≈ 4.5 ms at one wave per SIMD) longer than the GEMM chain it hides
+// under, so every chain waited ≈ 0.5 ms for it; same-box A/B of the HJB step (r03p): 1 → 5.23,
+// 2 → 5.09, 3 → 5.00–5.05, 4 → 5.07–5.11, 6 → 5.04–5.09, 8 → 5.12–5.13 ms.
+static int pis_prep_per_cu() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_PIS_PREP_PER_CU");
+    v = e ? std::max(1, std::min(8, std::atoi(e))) : 3;
+  }
+  return v;
+}
+
 // prepared: dpi_label_prepare already ran the first chunk's rollout and baseline rows (same
 // arguments, same workspace); prepare_only: run just those (dpi_label_prepare).
 static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
@@ -1145,11 +1158,12 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       return X3 ? pis_chain_x3(net->pis, rows, R, st, vjp) : pis_chain(net->pis, rows, R, st, vjp);
     };
     auto rollout = [&](int stage) {
-      // prepare stream: grids of one block per CU, so the rollout takes one wave per SIMD beside the
-      // previous batch's GEMM blocks instead of packing whole CUs (which starves the GEMM)
+      // prepare stream: grids of pis_prep_per_cu() blocks per CU, so the rollout takes a bounded share
+      // of each SIMD beside the previous batch's GEMM blocks instead of packing whole CUs (which
+      // starves the GEMM)
       int step = g;
       if (prepare_only) {
-        step = cu_count();
+        step = pis_prep_per_cu() * cu_count();
       }
       for (int bx0 = 0; bx0 < g; bx0 += step) {
         if (pis_rollout_unroll() == 4)
