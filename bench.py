@@ -399,15 +399,23 @@ def main():
         # at N GPUs is 512 points x 4096/N paths): profiles/<kind>_<workload>[_n<N>].json
         prof_tag = args.workload + (f"_n{world}" if "m_total" in wl and world > 1 else "")
         vf = ROOT / "profiles" / f"valu_{prof_tag}.json"
+        scale, busy_note = 1.0, ""
+        if not vf.exists() and prof_tag != args.workload:
+            # no PMC pass at this rank count: the N = 1 launch's busy cycles scaled by the path
+            # count (a rank's launch is the same kernel over M_PER_GPU / M of the paths, whole
+            # 64-path workgroups, so its VALU issue is proportional)
+            vf = ROOT / "profiles" / f"valu_{args.workload}.json"
+            scale = M_PER_GPU / M
+            busy_note = f", scaled by this rank's share of the paths ({M_PER_GPU}/{M})"
         if vf.exists() and not wl.get("pis"):
             kern = json.loads(vf.read_text())["kernels"]
             # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD>: the network launch, not the u = 0 twin
             net_k = [v for k, v in kern.items() if k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
-            busy = max(net_k, key=lambda v: v["dispatches"])["valu_busy_cycles_per_simd"]
+            busy = max(net_k, key=lambda v: v["dispatches"])["valu_busy_cycles_per_simd"] * scale
             valu = {"achieved": busy * N_SIMD / (k_ms * 1e-3) / 1e12, "peak": N_SIMD * PEAK_CLOCK_GHZ * 1e9 / 1e12,
                     "unit": "T VALU-busy SIMD-cycles/s", "valu_busy_cycles_per_simd": busy,
-                    "busy_source": f"profile_derived: profiles/valu_{prof_tag}.json (SQ_ACTIVE_INST_VALU x 4 / "
-                                   "1024 SIMDs per launch)"}
+                    "busy_source": f"profile_derived: {vf.relative_to(ROOT)} (SQ_ACTIVE_INST_VALU x 4 / "
+                                   f"1024 SIMDs per launch){busy_note}"}
             valu["frac"] = valu["achieved"] / valu["peak"]
         traffic = None
         tf = ROOT / "profiles" / f"traffic_{prof_tag}.json"
@@ -446,7 +454,7 @@ def main():
                                                                   if valu else
                                                                   {k: mfma[k] for k in ("achieved", "peak", "unit", "frac")}),
                          "traffic": traffic,
-                         "traffic_source": (f"profile_derived: profiles/traffic_{args.workload}.json (rocprofv3 PMC "
+                         "traffic_source": (f"profile_derived: profiles/traffic_{prof_tag}.json (rocprofv3 PMC "
                                             "FETCH_SIZE / WRITE_SIZE passes of this bench command, HBM bytes per "
                                             "label call)") if traffic is not None else None,
                          "hbm": hbm,
