@@ -83,6 +83,13 @@ static void launch(int kind, const Case& c, const Bufs& b, float* out) {
     const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
     hipLaunchKernelGGL(k_gemm_x3h<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
                        b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
+  } else if (kind == 5) {
+    const int nmt = (c.M + X3H_BM - 1) / X3H_BM, ntiles = nnt * nmt;
+    int ncu = 256;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    const int nb = std::min(ntiles, 2 * ncu);
+    hipLaunchKernelGGL(k_gemm_x3p<EPI>, dim3(nb), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, ntiles, b.W, 1.0f / 16.0f,
+                       b.X, c.ldx, b.X2, c.ldx2, c.nk1, out, c.Np, bias, b.AUX, c.ldaux);
   } else if (kind == 4) {
     const int nmt = (c.M + X3H_BM - 1) / X3H_BM;
     hipLaunchKernelGGL(k_gemm_x3t<EPI>, dim3(nnt * nmt), dim3(X3H_THREADS), 0, 0, c.M, c.Kp, nnt, b.W, 1.0f / 16.0f,
@@ -153,14 +160,14 @@ static void compare(const char* name, const Case& c, const Bufs& b, int iters, i
   launch<EPI>(0, c, b, b.REF);
   CK(hipDeviceSynchronize());
   for (int rep = 0; rep < reps; ++rep)
-    for (int kind : {1, 4}) {
+    for (int kind : {1, 5}) {
       CK(hipMemset(b.OUT, 0xFF, (size_t)c.M * c.Np * 4));
       const double us = timed<EPI>(kind, c, b, iters);
       const size_t bad = differing(c, b);
-      const double rel = kind == 4 ? max_rel(c, b) : 0.0;
+      const double rel = (kind == 4 || (kind == 5 && bad)) ? max_rel(c, b) : 0.0;
       std::printf("%-5s %-34s %-10s %8.1f us  %6.1f TF/s(split-eff)  differing words %zu  max rel diff %.2e\n",
                   EPI == EPI_DELU ? "delu" : "elu", name,
-                  kind == 0 ? "x3 (256)" : kind == 1 ? "x3h" : kind == 2 ? "x3q" : kind == 3 ? "x3e" : "x3t 32x32", us,
+                  kind == 0 ? "x3 (256)" : kind == 1 ? "x3h" : kind == 2 ? "x3q" : kind == 3 ? "x3e" : kind == 4 ? "x3t 32x32" : "x3p persist", us,
                   2.0 * c.M * (double)c.Kp * c.Np / (us * 1e-6) / 1e12, bad, rel);
       std::fflush(stdout);
     }

@@ -829,3 +829,227 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3t(int M, int Kp, int 
   }
 }
 }  // namespace dpi
+
+namespace dpi {
+// k_gemm_x3p: persistent k_gemm_x3h.  Two blocks per CU walk the tiles (virtual block v = b + k nb
+// takes the tile x3_tile_of_block would give block v of an ntiles-wide grid, so a block stays on
+// its XCD's tile range); between two tiles the next tile's chunks 0 and 1 are DMA'd into the ring
+// (both slots are free once every wave has read the last chunk) before the current tile's epilogue,
+// so the next tile's first wait is covered by the epilogue.  The bias double-buffers in LDS.  Waves
+// whose rows lie past M compute on the clamped last row (their stores are masked), so every wave
+// runs the same instruction stream and barriers.  Same products per output in the same order as
+// k_gemm_x3h: bitwise equal.
+// per-tile DMA state of k_gemm_x3p: the tile's base pointers and byte counts, the lane's offsets
+struct X3pTileDma {
+  const uint32_t* wb;
+  const float *xb, *x2b;
+  int xbytes, x2bytes;
+  int vw[4], vx[4], vx2[4];
+};
+__device__ __forceinline__ int x3p_tile(int v, int ntiles) {
+  const int xcd = v & 7, loc = v >> 3, q8 = ntiles >> 3;
+  return loc < q8 ? xcd * q8 + loc : 8 * q8 + xcd;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3p(int M, int Kp, int n_ntiles, int ntiles,
+                                                             const uint32_t* __restrict__ W, float wscale,
+                                                             const float* __restrict__ X, int ldx,
+                                                             const float* __restrict__ X2, int ldx2, int nk1,
+                                                             float* __restrict__ OUT, int ldc,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ AUX, int ldaux) {
+  constexpr int NT = 4, BN = 128, BM = X3H_BM, STAGE = X3HLds::STAGE, NWAVE = X3H_THREADS / 64;
+  constexpr int PER_WAVE = (BN + BM) / 8 / NWAVE;
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t sm[2 * STAGE + 2 * BN];  // the ring, then two bias slots
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int il = lane & 15, ql = lane >> 4;
+  const int nk = Kp >> 5;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int nb = gridDim.x;
+  auto tile_rsrc = [](const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  // per-tile DMA state: resources based at the tile, lane offsets (rows clamped to the tile's rows)
+  auto setup = [&](int t, X3pTileDma& d) {
+    const int mt = t / n_ntiles, m0 = mt * BM, n0 = (t - mt * n_ntiles) * BN;
+    const int mrows = min(BM, M - m0);
+    d.wb = W + (size_t)n0 * Kp;
+    d.xb = X + (size_t)m0 * ldx;
+    d.x2b = X2 + (size_t)m0 * ldx2;
+    d.xbytes = mrows * ldx * 4;
+    d.x2bytes = mrows * ldx2 * 4;
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+      const int w = k * NWAVE + wv;
+      const int r = 8 * w + (lane >> 3);
+      const int g = (lane & 7) ^ x3_swz(r);
+      if (k < PER_WAVE / 2) {
+        d.vw[k] = r * Kp * 4 + 16 * g;
+      } else {
+        const int xr = min(r - BN, mrows - 1);
+        d.vx[k - PER_WAVE / 2] = xr * ldx * 4 + 16 * g;
+        d.vx2[k - PER_WAVE / 2] = xr * ldx2 * 4 + 16 * g;
+      }
+    }
+  };
+  auto issue = [&](const X3pTileDma& d, int c, int slot) {
+    uint32_t* dst = sm + slot * STAGE;
+    const bool one = c < nk1;
+    const int sx = one ? 128 * c : 128 * (c - nk1);
+    const __amdgpu_buffer_rsrc_t rw = tile_rsrc(d.wb, (size_t)BN * Kp * 4);
+    const __amdgpu_buffer_rsrc_t rx = one ? tile_rsrc(d.xb, d.xbytes) : tile_rsrc(d.x2b, d.x2bytes);
+#pragma unroll
+    for (int k = 0; k < PER_WAVE; ++k) {
+      __attribute__((address_space(3))) void* p =
+          (__attribute__((address_space(3))) void*)(dst + 256 * (k * NWAVE + wvu));
+      if (k < PER_WAVE / 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, p, 16, d.vw[k], 128 * c, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, p, 16, one ? d.vx[k - PER_WAVE / 2] : d.vx2[k - PER_WAVE / 2],
+                                                 sx, 0, 0);
+    }
+  };
+  auto frag = [&](const uint32_t* buf, int row, h8& h, h8& l) {
+    const int s = x3_swz(row);
+    const uint32_t* rp = buf + row * 32;
+    h = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql) ^ s)));
+    l = __builtin_bit_cast(h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql + 1) ^ s)));
+  };
+  f4v acc[NT][4];
+  h8 ah[2][NT], al[2][NT], bh[2][4], bl[2][4];
+  auto load = [&](int slot, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    const uint32_t* buf = sm + slot * STAGE;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) frag(buf, wn * 16 * NT + 16 * t + il, ah[F][t], al[F][t]);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) frag(buf, BN + wm * 64 + 16 * b + il, bh[F][b], bl[F][b]);
+  };
+  auto mma = [&](auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[F][t], bl[F][b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[F][t], bh[F][b], acc[t][b], 0, 0, 0);
+      }
+  };
+  X3pTileDma cur;
+  auto body = [&](int u, auto Fc) {
+    constexpr int F = decltype(Fc)::value;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (u + 2 < nk) issue(cur, u + 2, u & 1);
+    load((u + 1) & 1, std::integral_constant<int, F ^ 1>{});
+    mma(Fc);
+    constexpr int NRD = 2 * (NT + 4), NMF = 3 * NT * 4;
+#pragma unroll
+    for (int i = 0; i < NRD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NMF / NRD, 0);
+    }
+  };
+  const bool has_bias = (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && bias != nullptr;
+  __builtin_amdgcn_s_setprio(2);
+  int v = blockIdx.x;
+  if (v >= ntiles) return;  // (the host launches at most ntiles blocks)
+  int tile = x3p_tile(v, ntiles);
+  setup(tile, cur);
+  // first tile's prologue: bias slot 0, chunks 0 and 1
+  {
+    const int n0 = (tile % n_ntiles) * BN;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (has_bias && tid < BN / 4) bv = *reinterpret_cast<const float4*>(bias + n0 + 4 * tid);
+    issue(cur, 0, 0);
+    if (nk > 1) issue(cur, 1, 1);
+    if (has_bias && tid < BN / 4) *reinterpret_cast<float4*>(reinterpret_cast<float*>(sm + 2 * STAGE) + 4 * tid) = bv;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  for (int k = 0;; ++k) {
+    const int mt = tile / n_ntiles, m0 = mt * BM, n0 = (tile - mt * n_ntiles) * BN;
+    const float* sbias = reinterpret_cast<const float*>(sm + 2 * STAGE) + (k & 1) * BN;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[t][b] = f4v{0.f, 0.f, 0.f, 0.f};
+    load(0, std::integral_constant<int, 0>{});
+    int u = 0;
+    for (; u + 2 < nk; u += 2) {
+      body(u, std::integral_constant<int, 0>{});
+      body(u + 1, std::integral_constant<int, 1>{});
+    }
+    if (u + 1 < nk) {
+      body(u, std::integral_constant<int, 0>{});
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      mma(std::integral_constant<int, 1>{});
+    } else {
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      mma(std::integral_constant<int, 0>{});
+    }
+    // every wave's fragment reads of both slots retired: the ring is free for the next tile
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int vn = v + nb;
+    const bool more = vn < ntiles;
+    int tile_n = tile;
+    if (more) {
+      tile_n = x3p_tile(vn, ntiles);
+      setup(tile_n, cur);
+      issue(cur, 0, 0);
+      if (nk > 1) issue(cur, 1, 1);
+      if (has_bias && tid < BN / 4) {
+        const int nn0 = (tile_n % n_ntiles) * BN;
+        const float4 bv = *reinterpret_cast<const float4*>(bias + nn0 + 4 * tid);
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(sm + 2 * STAGE) + ((k + 1) & 1) * BN + 4 * tid) = bv;
+      }
+    }
+    // epilogue of this tile (as k_gemm_x3h), under the next tile's first DMA
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = m0 + wm * 64 + 16 * b + il;
+      if (m >= M) continue;
+#pragma unroll
+      for (int c = 0; c < NT / 2; ++c) {
+        const int U = (n0 >> 5) + wn * (NT / 2) + c;
+        float vv[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vv[r] = acc[2 * c][b][r] * wscale;
+          vv[4 + r] = acc[2 * c + 1][b][r] * wscale;
+        }
+        if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
+          if (has_bias) {
+            const float* bsrc = sbias + 32 * (wn * (NT / 2) + c) + 4 * ql;
+            const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+            const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
+            vv[0] += b0.x, vv[1] += b0.y, vv[2] += b0.z, vv[3] += b0.w;
+            vv[4] += b1.x, vv[5] += b1.y, vv[6] += b1.z, vv[7] += b1.w;
+          }
+          if (EPI == EPI_BIAS_ELU)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vv[j] = vv[j] > 0.f ? vv[j] : __expf(vv[j]) - 1.0f;
+        } else {
+          float a[8];
+          x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) vv[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
+        }
+        x3_put8(OUT + (size_t)m * ldc, 0, U, ql, vv);
+      }
+    }
+    if (!more) break;
+    // the next tile's chunks 0 and 1 and its bias landed; every wave is past this tile's epilogue
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    v = vn;
+    tile = tile_n;
+  }
+}
+}  // namespace dpi
