@@ -211,8 +211,8 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
 
 // Block bx0 + blockIdx.x of the chunk.  8.7 KB of LDS (no staging of X_s); UNR independent Philox
 // chains per wave in the noise loops, capped at 64 VGPRs, so a rollout block (one wave per SIMD)
-// fits on a CU beside two k_gemm_x3h blocks (2 x 66 KB, 2 x 224 VGPRs per SIMD): the prepare stream
-// launches the next batch's rollout in grids of one block per CU.
+// fits on a CU beside two k_gemm_x3h blocks (2 x 66 KB, 2 x 208 VGPRs per SIMD): the prepare stream
+// launches the next batch's rollout in grids of DPI_PIS_PREP_PER_CU (3) blocks per CU.
 template <int KIND, bool X3, int UNR = 2>
 __global__ __launch_bounds__(256, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                      int nbp, int m_begin, int K, int flags, uint32_t k0,
