@@ -117,3 +117,39 @@ def test_gbm_hessian_labels_config4_full_size():
                       _rel(y[i:i + 1, 101:], ref[:, 101:]))
         print(f"point {i}: value {ev:.2e} grad {eg:.2e} hessian {eh:.2e}")
         assert ev < TOL and eg < TOL and eh < TOL, (i, ev, eg, eh)
+
+
+def test_hjb_two_pipeline_chunks_equal_separate_calls():
+    """More (point, path-block) pairs than one PISGradNet pipeline chunk holds (66 points x 4096 paths
+    = 4,224 pairs > DPI_PIS_CHUNK's 4,096): the second chunk's rows (points 64 and 65) run a second
+    rollout -> GEMM chain -> final pass, with the baseline rows of all 66 points riding in the first
+    chunk.  A row's result does not depend on where it sits in a chunk, so the two-chunk call equals
+    the one-chunk calls over points 0-63 and 64-65 (same global point indices) bit for bit; the
+    last point matches the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    from oracle import dpi_oracle as O
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(0)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    n, M, K = 66, 4096, 50
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    full = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, gen.point_baseline(tx))
+    a = tx[:64].contiguous()
+    b = tx[64:].contiguous()
+    part_a = gen.label_moments(a, 0, M, 0, M, L.DPI_BOTH, gen.point_baseline(a))
+    part_b = gen.label_moments(b, 64, M, 0, M, L.DPI_BOTH, gen.point_baseline(b))
+    assert torch.equal(full[:64], part_a)
+    assert torch.equal(full[64:], part_b)
+    ws = gen.point_baseline(tx)
+    y = gen.finalize(gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws), M, L.DPI_BOTH, ws).cpu().double().numpy()
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    txh = tx.cpu().double().numpy()
+    ref = O.labels_grad(oeq, onet, txh[n - 1:n], M, K, 1, 1, n - 1, m_chunk=512)
+    ev, eg = _rel(y[n - 1:n, :1], ref[:, :1]), _rel(y[n - 1:n, 1:], ref[:, 1:])
+    print(f"point {n - 1} (second chunk): value {ev:.2e} grad {eg:.2e}")
+    assert ev < TOL and eg < TOL, (ev, eg)
