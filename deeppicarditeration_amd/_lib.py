@@ -18,6 +18,7 @@ DPI_ACT_ELU = 1
 DPI_TERMINAL, DPI_INTEGRAL, DPI_BOTH = 1, 2, 3
 DPI_PREPARED = 4  # dpi_label_moments: dpi_label_prepare already ran with the same arguments
 DPI_PATH_BLOCK = 64
+DPI_PATHS_PER_CALL_MAX = 1024 * DPI_PATH_BLOCK
 DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
 DPI_STATUS_NONFINITE = 1
 

@@ -1247,7 +1247,7 @@ static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   if (n == 0) return 0;
   const int F = 1 + p->e.nx;
   const int nbp = (m_end - m_begin) / P;
-  if (nbp > 1024) return fail(DPI_ERR_ARG, "label_moments: at most 1024 x 64 paths per call");
+  if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "label_moments: at most DPI_PATHS_PER_CALL_MAX paths per call");
   *w = ws_layout(net, n, M, F);
   if (ws_bytes < w->total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
@@ -1458,7 +1458,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
     return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
   if (n == 0) return 0;
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
-  if (nbp > 1024) return fail(DPI_ERR_ARG, "Hessian labels: at most 1024 x 64 paths per call");
+  if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "Hessian labels: at most DPI_PATHS_PER_CALL_MAX paths per call");
   const WsLayout w = ws_layout(net, n, M, F);
   size_t moff;
   const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);

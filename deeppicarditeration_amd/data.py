@@ -29,6 +29,9 @@ from .dataset import IterableDatasetWithInternalBatch
 from .equations import Equation, OUProcessEquation, SimpleDiffusionEquation, SimpleDiffusionEquationWithHessian
 from .solution import DeviceNet
 
+# paths one label call takes (include/dpi.h DPI_PATHS_PER_CALL_MAX); more run as several calls
+PATHS_PER_CALL_MAX = _lib.DPI_PATHS_PER_CALL_MAX
+
 
 def _ptr(t):
     return _lib.c_void_p(t.data_ptr())
@@ -307,8 +310,24 @@ class OnlineDataGenerator:
                                                _stream(self._device)), "dpi_point_baseline")
         return ws
 
+    def _pieces(self, m_begin, m_end, flags=0):
+        """[m_begin, m_end) cut into ranges one C-ABI call takes (at most PATHS_PER_CALL_MAX paths)."""
+        if m_end - m_begin <= PATHS_PER_CALL_MAX:
+            return [(m_begin, m_end)]
+        if flags & _lib.DPI_PREPARED:
+            raise ValueError(f"a prepared label call covers at most {PATHS_PER_CALL_MAX} paths")
+        return [(a, min(a + PATHS_PER_CALL_MAX, m_end)) for a in range(m_begin, m_end, PATHS_PER_CALL_MAX)]
+
     def label_moments(self, tx, point_base, M, m_begin, m_end, flags, ws):
-        """Sum / sum-of-squares of per-path contributions over m in [m_begin, m_end): (n, 2, 1+nx)."""
+        """Sum / sum-of-squares of per-path contributions over m in [m_begin, m_end): (n, 2, 1+nx).
+        More than PATHS_PER_CALL_MAX paths run as several calls combined by moments_reduce."""
+        pieces = self._pieces(m_begin, m_end, flags)
+        if len(pieces) > 1:
+            return self.moments_reduce(torch.stack([self._label_moments(tx, point_base, M, a, b, flags, ws)
+                                                    for a, b in pieces]))
+        return self._label_moments(tx, point_base, M, m_begin, m_end, flags, ws)
+
+    def _label_moments(self, tx, point_base, M, m_begin, m_end, flags, ws):
         n = tx.shape[0]
         mom = torch.empty(n, 2, 1 + self.equation.nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
@@ -349,7 +368,16 @@ class OnlineDataGenerator:
         return y
 
     def label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
-        """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2)."""
+        """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2).
+        More than PATHS_PER_CALL_MAX paths run as several calls combined by sums_reduce."""
+        pieces = self._pieces(m_begin, m_end)
+        if len(pieces) > 1:
+            parts = [self._label_moments_hessians(tx, point_base, M, a, b, ws) for a, b in pieces]
+            return (self.sums_reduce(torch.stack([p[0] for p in parts])),
+                    self.sums_reduce(torch.stack([p[1] for p in parts])))
+        return self._label_moments_hessians(tx, point_base, M, m_begin, m_end, ws)
+
+    def _label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
         n, nx = tx.shape[0], self.equation.nx
         mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self._device)
         hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self._device)
@@ -420,6 +448,10 @@ class OnlineDataGenerator:
         if self.n_estimate_terminal != self.n_estimate_integral:
             raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
         n, nx, M = tx.shape[0], self.equation.nx, self.n_estimate_integral
+        if M > PATHS_PER_CALL_MAX:  # several calls: baseline, per-range sums, one finalize
+            ws = self.point_baseline(tx, hessians=True)
+            mom, hs = self.label_moments_hessians(tx, pb, M, 0, M, ws)
+            return self.finalize_hessians(mom, hs, M, ws, bound)
         need = self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self._device)
@@ -441,7 +473,7 @@ class OnlineDataGenerator:
 
     def _generate_once(self, tx, pb, flags, bound=None):
         MT, MI = self.n_estimate_terminal, self.n_estimate_integral
-        if MT == MI or flags != _lib.DPI_BOTH:
+        if (MT == MI or flags != _lib.DPI_BOTH) and max(MT, MI) <= PATHS_PER_CALL_MAX:
             # one C-ABI call: baseline + fused rollout/label kernel + block reduce/finalize
             M = MT if flags == _lib.DPI_TERMINAL else MI
             n = tx.shape[0]
@@ -455,6 +487,10 @@ class OnlineDataGenerator:
                 _ptr(self.last_moments), _ptr(ws), ws.numel(), _stream(self._device)), "dpi_generate_with_gradients")
             return y
         ws = self.point_baseline(tx)
+        if MT == MI or flags != _lib.DPI_BOTH:  # one estimator set over more paths than one call takes
+            M = MT if flags == _lib.DPI_TERMINAL else MI
+            self.last_moments = self.label_moments(tx, pb, M, 0, M, flags, ws)
+            return self.finalize(self.last_moments, M, flags, ws, bound)
         yT = self.finalize(self.label_moments(tx, pb, MT, 0, MT, _lib.DPI_TERMINAL, ws), MT, _lib.DPI_TERMINAL, ws,
                            float("inf"))
         yI = self.finalize(self.label_moments(tx, pb, MI, 0, MI, _lib.DPI_INTEGRAL, ws), MI, _lib.DPI_INTEGRAL, ws,

@@ -77,6 +77,8 @@ extern "C" {
 
 /* Monte-Carlo paths per workgroup: m ranges are multiples of this. */
 #define DPI_PATH_BLOCK 64
+/* paths (m_end - m_begin) one label-moments call takes: 1024 path blocks per point */
+#define DPI_PATHS_PER_CALL_MAX 65536
 
 typedef struct dpi_problem_s* dpi_problem;
 typedef struct dpi_net_s* dpi_net;

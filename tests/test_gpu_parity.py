@@ -612,3 +612,45 @@ def test_prepared_moments_check_the_prepare_call():
     ref = gen.label_moments(tx, pb, 128, 0, 128, L.DPI_BOTH, gen.point_baseline(tx))
     torch.cuda.synchronize()
     assert torch.equal(mom, ref)
+
+
+@pytest.mark.parametrize("hessians", [False, True])
+def test_more_paths_than_one_call_takes(hessians):
+    """M = 131,072 > DPI_PATHS_PER_CALL_MAX: the generator runs two label calls over [0, 65536) and
+    [65536, 131072) and combines them (moments_reduce / sums_reduce), so reference-sized settings
+    beyond one call's 1,024 path blocks work; the labels match the fp64 oracle on the same counters."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    from oracle import dpi_oracle as O
+    M, K = 2 * L.DPI_PATHS_PER_CALL_MAX, 4
+    if hessians:
+        eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+        torch.manual_seed(3)
+        net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+        oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+        act = ["ELU"] * 3
+    else:
+        eq = dpi.Cha(nx=100, T=1.0, k=5.0, alpha=1.0)
+        torch.manual_seed(0)
+        net = dpi.construct_mlp(101, 1, [32] * 2, ["ELU"] * 2, None)
+        oeq = O.Cha(100, 1.0, 5.0, 1.0)
+        act = ["ELU"] * 2
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=K, seed=1)
+    tx, _ = gen.sample_t_and_x(1, point_base=0)
+    y = (gen.generate_with_gradients_and_hessians(tx, point_base=0) if hessians
+         else gen.generate_with_gradients(tx, point_base=0)).cpu().double().numpy()
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin], act)
+    txh = tx.cpu().double().numpy()
+    ref = (O.labels_grad_hess(oeq, onet, txh, M, K, 1, 1, 0, m_chunk=4096) if hessians
+           else O.labels_grad(oeq, onet, txh, M, K, 1, 1, 0, m_chunk=4096))
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    ev, eg = rel(y[:, :1], ref[:, :1]), rel(y[:, 1:101], ref[:, 1:101])
+    print(f"M = {M}: value {ev:.2e} grad {eg:.2e}")
+    assert ev < 1e-4 and eg < 1e-4
+    if hessians:
+        eh = rel(y[:, 101:], ref[:, 101:])
+        print(f"hessian {eh:.2e}")
+        assert eh < 1e-4
