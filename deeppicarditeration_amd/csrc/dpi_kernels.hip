@@ -20,6 +20,7 @@
 #include "dpi_rng.h"
 
 #include "dpi_dispatch.h"
+#include "dpi_pisnet.h"
 
 namespace dpi {
 
@@ -192,6 +193,25 @@ static int upload(dpi_problem_s* p, const std::vector<T>& v, const T** out) {
 
 // The same fragment order for the split-storage GEMM (k_gemm_x3, dpi_gemm.h): x' = 2^s x with
 // max |x'| in [0.5, 1), hi = fp16(x'), lo = fp16(x' - hi) (unscaled).  *wscale = 2^-s.
+
+// Fragment-major copy of a packed split matrix (R rows of C words, R % 16 == 0, C % 32 == 0) for
+// k_pis_net: block (T, c) of 512 words = lane l's hi granule (row 16 T + l % 16, words
+// 32 c + 8 (l / 16) .. + 3) at 4 l, then its lo granule (the next 4 words) at 256 + 4 l.
+static size_t pack_frag_major(std::vector<float>& blob, size_t src, int R, int C) {
+  blob.resize((blob.size() + 31) & ~size_t(31), 0.f);
+  const size_t off = blob.size();
+  blob.resize(off + (size_t)R * C, 0.f);
+  const int nc = C / 32;
+  for (int T = 0; T < R / 16; ++T)
+    for (int c = 0; c < nc; ++c)
+      for (int h = 0; h < 2; ++h)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 4; ++j)
+            blob[off + (((size_t)T * nc + c) * 2 + h) * 256 + 4 * l + j] =
+                blob[src + (size_t)(16 * T + (l & 15)) * C + 32 * c + 8 * (l >> 4) + 4 * h + j];
+  return off;
+}
+
 template <class F>
 static size_t pack_split_x3(std::vector<float>& blob, int R, int C, F at, float* wscale) {
   float mx = 0.f;
@@ -627,6 +647,7 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
   int hp[4];
   for (int l = 0; l < L; ++l) hp[l] = r64(hidden[l]);
   size_t s_te0, s_te2, s_sn0, s_sn[4] = {0}, s_nn[5] = {0}, s_nnT[5] = {0}, s_nnbP[5] = {0}, s_gxno = 0;
+  size_t s_nnF[5] = {0}, s_nnTF[5] = {0}, s_gxnoF = 0;
   float w_te0 = 1.f, w_te2 = 1.f, w_sn0 = 1.f, w_sn[4] = {1.f, 1.f, 1.f, 1.f}, w_nn[5], w_nnT[5], w_gxno = 1.f;
   {
     auto align = [&]() { blob.resize((blob.size() + 31) & ~size_t(31), 0.f); };
@@ -667,6 +688,11 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
         return k < inl ? wl[(size_t)d * inl + k] : 0.f;
       }, &w_gxno);
     }
+    for (int l = 0; l <= L; ++l) {
+      s_nnF[l] = pack_frag_major(blob, s_nn[l], l < L ? hp[l] : NOP, l == 0 ? INP : hp[l - 1]);
+      s_nnTF[l] = pack_frag_major(blob, s_nnT[l], l == 0 ? NOP : hp[l - 1], l == 0 ? hp[0] : l == L ? NXK : hp[l]);
+    }
+    s_gxnoF = pack_frag_major(blob, s_gxno, NOP, hp[0] + hp[L - 1]);
     for (int l = 0; l <= L; ++l) {
       const int o = l < L ? hidden[l] : nx, op = l < L ? hp[l] : NOP;
       align();
@@ -718,10 +744,13 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
     pd.te0W = w_te0, pd.te2W = w_te2, pd.sn0W = w_sn0;
     for (int j = 0; j < nsm; ++j) pd.snS[j] = u32(s_sn[j]), pd.snW[j] = w_sn[j];
     pd.gxnoS = u32(s_gxno);
+    pd.gxnoF = u32(s_gxnoF);
     pd.gxnoW = w_gxno;
     for (int l = 0; l <= L; ++l) {
       pd.nnS[l] = u32(s_nn[l]);
       pd.nnTS[l] = u32(s_nnT[l]);
+      pd.nnF[l] = u32(s_nnF[l]);
+      pd.nnTF[l] = u32(s_nnTF[l]);
       pd.nnW[l] = w_nn[l];
       pd.nnTW[l] = w_nnT[l];
       pd.nnbP[l] = base + s_nnbP[l];
@@ -946,6 +975,21 @@ static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws,
     gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, st);
 }
 
+// k_pis_net (the fused split VJP chain) by default; DPI_PIS_FUSED=0 selects the layer-wise
+// k_gemm_x3h chain (read per call, so one process can compare both).
+static bool pis_fused_on() {
+  const char* e = std::getenv("DPI_PIS_FUSED");
+  return !e || std::atoi(e) != 0;
+}
+// k_pis_net's shapes: 1-4 hidden layers of 512 units, nx <= 128 (X in <= 4 chunks, GX 64 or 128 wide)
+static bool pis_fused_fits(const NetPisDev& pd, const PisRows& L) {
+  if (pd.L < 1 || pd.L > 4) return false;
+  for (int l = 0; l < pd.L; ++l)
+    if (pd.h[l] != PN_H) return false;
+  const int nxk = L.INP / 32 - 2, nop = (pd.nx + 63) & ~63;
+  return nxk >= 1 && nxk <= PN_XC && (nop == 64 || nop == 128);
+}
+
 // The PISGradNet chain of pis_chain in split storage (every width padded to 32; the x part of IN
 // starts at its chunk 2 = word 64).
 static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t st, bool vjp = true) {
@@ -957,6 +1001,15 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
     const int ncu = cu_count();
     const int blocks = std::max(1, std::min(ncu, (R + 16 * (PT_THREADS / 64) - 1) / (16 * (PT_THREADS / 64))));
     hipLaunchKernelGGL(k_pis_time<4>, dim3(blocks), dim3(PT_THREADS), 0, st, pd, rows, L, R);
+  }
+  // the VJP chain as one launch with the activations in LDS (dpi_pisnet.h), where the shape fits
+  if (vjp && R > 0 && pis_fused_on() && pis_fused_fits(pd, L)) {
+    const dim3 grid((R + PN_BM - 1) / PN_BM), block(PN_THREADS);
+    if (NOP == 128)
+      hipLaunchKernelGGL(k_pis_net<2>, grid, block, 0, st, pd, rows, L, R);
+    else
+      hipLaunchKernelGGL(k_pis_net<1>, grid, block, 0, st, pd, rows, L, R);
+    return L;
   }
   int Kp = L.INP;
   const float* a = rows + L.IN;

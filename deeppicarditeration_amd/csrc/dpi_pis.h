@@ -45,6 +45,10 @@ struct NetPisDev {
   const float* nnbP[5];
   // [nnT[0] | nn[L]] ((nx -> 64) x (h_0 + h_{L-1})): J^T X + net_out = [D_0 | A_{L-1}] . this^T + b_L
   const uint32_t* gxnoS;
+  // fragment-major copies for k_pis_net (dpi_pisnet.h): per 16-row tile T and 32-deep chunk c a
+  // 2 KB block, the 64 lanes' hi granules (lane l: row 16 T + l % 16, granule pair l / 16) then
+  // their lo granules, so each weight-fragment load is one contiguous 1 KB (8 whole lines)
+  const uint32_t *nnF[5], *nnTF[5], *gxnoF;
   // k_gemm_x3 weight scales 2^-s (each split matrix is stored prescaled by 2^s)
   float te0W, te2W, sn0W, snW[4], nnW[5], nnTW[5], gxnoW;
 };

@@ -1,0 +1,321 @@
+// k_pis_net: the whole split-storage PISGradNet nn_module chain of pis_chain_x3 (solution.py:256-289)
+// in ONE launch, 64 rows per block, with the 512-wide activations held in LDS across layers.
+//
+// pis_chain_x3 runs the chain as 9 k_gemm_x3h launches; between launches every 512-wide activation
+// and cotangent makes an HBM round trip (13 GB per HJB label call, profiles/traffic_hjb.json) and
+// every launch pays its tiles' prologues and epilogues.  Here a block takes 64 rows through
+//   forward   A_l = elu(W_l A_{l-1} + b_l)                       l = 0 .. L-1  (A_{-1} = IN)
+//   VJP       D_{L-1} = (nnT[L] X) * elu'(A_{L-1}),  D_{l-1} = (nnT[l] D_l) * elu'(A_{l-1})
+//   output    GX = [D_0 | A_{L-1}] . [nnT[0] | nn[L]]^T + b_L
+// with the current 512-wide operand in a 128 KB LDS image (64 rows x 16 chunks, chunk-major so each
+// 32-deep chunk is a 64-row slab laid out like a k_gemm_x3h ring slot) and the x part of IN in a
+// 32 KB image: 160 KB, one block (8 waves, 2 per SIMD) per CU.  Only A_0 .. A_{L-1} go to HBM (the
+// VJP's elu' operands and the second half of GX's K), and GX; nothing else leaves the CU.
+//
+// Wave w owns units 64 w .. 64 w + 63 of every 512-wide product: its weight rows are private, so the
+// MFMA A operands come straight from global (L2-resident: 1 MB per layer shared by every block) into
+// registers as buffer loads, one chunk ahead; the B operands (the 64 rows) are the shared LDS image.
+// Per chunk and output the same three products in the same order as k_gemm_x3h (hi.hi, hi.lo,
+// lo.hi into one accumulator), the same epilogue arithmetic and the same split on store, so every
+// row's GX is bitwise equal to the layer-wise chain (tests/test_gpu_parity.py).
+#pragma once
+
+namespace dpi {
+
+constexpr int PN_BM = 64, PN_THREADS = 512, PN_SLAB = PN_BM * 32;  // words per 32-deep chunk slab
+constexpr int PN_H = 512, PN_HC = PN_H / 32;                       // hidden width and its chunks
+constexpr int PN_XC = 4;                                           // chunks of the x part of IN (nx <= 128)
+
+struct PnLds {
+  uint32_t act[PN_HC * PN_SLAB];  // 128 KB: the current 512-wide operand
+  uint32_t xs[PN_XC * PN_SLAB];   // 32 KB: X = IN[:, 64:]
+};
+
+typedef _Float16 pn_h8 __attribute__((ext_vector_type(8)));
+typedef float pn_f4 __attribute__((ext_vector_type(4)));
+
+// LDS writes retired, then the workgroup barrier; the memory clobber keeps the compiler from moving
+// LDS accesses across it.  (Not __syncthreads(): its vmcnt(0) would also wait for the weight loads
+// and HBM stores in flight.)
+__device__ __forceinline__ void pn_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pn_rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// fragment (hi, lo) of row `row` of a slab, lane group ql (x3_swz-swizzled granules, as k_gemm_x3h)
+__device__ __forceinline__ void pn_frag(const uint32_t* slab, int row, int ql, pn_h8& h, pn_h8& l) {
+  const int s = x3_swz(row);
+  const uint32_t* rp = slab + row * 32;
+  h = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql) ^ s)));
+  l = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(rp + 4 * ((2 * ql + 1) ^ s)));
+}
+
+// split x = hi + lo of the 8 values of one granule pair (x3_put8's arithmetic)
+__device__ __forceinline__ void pn_split8(const float (&v)[8], u32x4_t& h, u32x4_t& l) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t hw = 0, lw = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float x = v[2 * p + e];
+      const _Float16 hi = (_Float16)x;
+      const _Float16 lo = (_Float16)(x - (float)hi);
+      hw |= (uint32_t)__builtin_bit_cast(uint16_t, hi) << (16 * e);
+      lw |= (uint32_t)__builtin_bit_cast(uint16_t, lo) << (16 * e);
+    }
+    h[p] = hw;
+    l[p] = lw;
+  }
+}
+
+// acc[t][b] += sum over chunks c < nk of W[tile T0 + t][chunk c0 + c] . slab(c)[rows p0 + 16 b + il]
+// W: a fragment-major matrix (NetPisDev::nnF, pack_frag_major) with nkw chunks per row, behind the
+// buffer resource rw; every weight load is lane l's 16 B of a 1 KB block (one VGPR offset for all;
+// tile, chunk and hi / lo in the scalar offset).  The weights run NS - 1 chunks ahead in NS
+// register sets (the loop unrolled by NS, branch-free: loads past the last chunk repeat it), so a
+// load has NS - 1 chunks of MFMAs to arrive from L2; the B fragments (LDS) are read per chunk just
+// before its MFMAs.  Rows p0 + 16 b + il share x3_swz, so two LDS addresses serve every path tile.
+template <int NT, int NB, int NS, class Slab>
+__device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], __amdgpu_buffer_rsrc_t rw, int T0, int nkw, int c0, int nk,
+                                        int p0, int lane, int il, int ql, Slab slab) {
+  pn_h8 ah[NS][NT], al[NS][NT];
+  const int vo = 16 * lane;
+  const int sw = x3_swz(il);  // = x3_swz(p0 + 16 b + il): p0 % 16 == 0
+  const int oh = (p0 + il) * 32 + 4 * ((2 * ql) ^ sw), ol = (p0 + il) * 32 + 4 * ((2 * ql + 1) ^ sw);
+  auto ldw = [&](int c, auto Sc) {
+    constexpr int S = decltype(Sc)::value;
+    c = min(c, nk - 1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int so = ((T0 + t) * nkw + c0 + c) * 2048;
+      ah[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so, 0));
+      al[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so + 1024, 0));
+    }
+  };
+  auto mm = [&](int c, auto Sc) {
+    constexpr int S = decltype(Sc)::value;
+    const uint32_t* s = slab(c);
+    pn_h8 bh[NB], bl[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      bh[b] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + oh + 512 * b));
+      bl[b] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + ol + 512 * b));
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[S][t], bh[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[S][t], bl[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[S][t], bh[b], acc[t][b], 0, 0, 0);
+      }
+  };
+  static_assert(NS == 3, "the rotation below is written for three sets");
+  constexpr std::integral_constant<int, 0> I0{};
+  constexpr std::integral_constant<int, 1> I1{};
+  constexpr std::integral_constant<int, 2> I2{};
+  // sched_barrier(0): the scheduler keeps each load group where it is written (left alone it sinks
+  // every load next to its first use to shorten live ranges)
+  ldw(0, I0);
+  ldw(1, I1);
+  int c = 0;
+#pragma unroll 1
+  for (; c + 3 <= nk; c += 3) {
+    ldw(c + 2, I2);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(c, I0);
+    __builtin_amdgcn_sched_barrier(0);
+    ldw(c + 3, I0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(c + 1, I1);
+    __builtin_amdgcn_sched_barrier(0);
+    ldw(c + 4, I1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(c + 2, I2);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (c < nk) mm(c, I0);
+  if (c + 1 < nk) mm(c + 1, I1);
+}
+
+template <int NT, int NB>
+__device__ __forceinline__ void pn_zero(pn_f4 (&acc)[NT][NB]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[t][b] = pn_f4{0.f, 0.f, 0.f, 0.f};
+}
+
+enum { PN_ELU = 0, PN_DELU_LDS = 1, PN_DELU_HBM = 2 };
+
+// NB_GX: path tiles per wave of the GX product (NOP = 128: 4 unit groups of 32 x 2 path groups;
+// NOP = 64: 2 x 4).  R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.
+template <int NB_GX>
+__global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* __restrict__ rows, PisRows L, int R) {
+  __shared__ PnLds lds;
+  const int tid = threadIdx.x, lane = tid & 63, il = lane & 15, ql = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = blockIdx.x * PN_BM, mrows = min(PN_BM, R - m0);
+  const size_t ld = (size_t)L.stride;
+  const int nxk = L.INP / 32 - 2;  // chunks of X (1 .. PN_XC; host-checked)
+  float* const rbase = rows + (size_t)m0 * ld;
+  // above any co-resident wave of another kernel, as the layer-wise GEMMs
+  __builtin_amdgcn_s_setprio(2);
+  auto act = [&](int c) -> uint32_t* { return lds.act + c * PN_SLAB; };
+  auto xsl = [&](int c) -> uint32_t* { return lds.xs + c * PN_SLAB; };
+  // thread tid moves granule tid & 7 of tile row tid >> 3 in each chunk of a row region
+  const int gr = tid >> 3, gg = tid & 7;
+  const int grc = min(gr, mrows - 1);  // rows past R load the last row (results discarded)
+  auto gsrc = [&](int reg, int c) {
+    return reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint32_t*>(rbase + (size_t)grc * ld + reg) + 32 * c +
+                                            4 * gg);
+  };
+  auto gdst = [&](uint32_t* slab) { return reinterpret_cast<u32x4_t*>(slab + gr * 32 + 4 * (gg ^ x3_swz(gr))); };
+
+  // IN: the time embedding (chunks 0, 1) -> act, X (chunks 2 ..) -> xs
+  {
+    u32x4_t v[2 + PN_XC];
+#pragma unroll
+    for (int c = 0; c < 2 + PN_XC; ++c)
+      if (c < 2 + nxk) v[c] = *gsrc(L.IN, c);
+#pragma unroll
+    for (int c = 0; c < 2 + PN_XC; ++c)
+      if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
+  }
+  pn_barrier();
+
+  // the 512-wide products: wave wv owns units 64 wv .. 64 wv + 63 (4 unit tiles) of all 64 rows
+  pn_f4 acc[4][4];
+  // a fragment-major weight matrix of `rows` rows and Kp words per row
+  auto wsrc = [&](const uint32_t* W, int rows_, int Kp) { return pn_rsrc(W, (size_t)rows_ * Kp * 4); };
+  // epilogue of a 512-wide product: lane (il, ql) of path tile b holds units 64 wv + 16 t + 4 ql + r
+  // of row 16 b + il; unit tiles (2 c, 2 c + 1) form granule pair ql of chunk U = 2 wv + c
+  auto epilogue = [&](int kind, float ws, const float* bias, int save_reg, int aux_reg) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int m = 16 * b + il;
+      const int s = x3_swz(m);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int U = 2 * wv + c;
+        u32x4_t* lh = reinterpret_cast<u32x4_t*>(act(U) + m * 32 + 4 * ((2 * ql) ^ s));
+        u32x4_t* ll = reinterpret_cast<u32x4_t*>(act(U) + m * 32 + 4 * ((2 * ql + 1) ^ s));
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * c][b][r] * ws;
+          v[4 + r] = acc[2 * c + 1][b][r] * ws;
+        }
+        if (kind == PN_ELU) {
+          const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
+          const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql + 16);
+          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+        } else {
+          u32x4_t h, l;
+          if (kind == PN_DELU_LDS) {  // elu' of A_{L-1}, still in this wave's own granules
+            h = *lh;
+            l = *ll;
+          } else {
+            const u32x4_t* g = reinterpret_cast<const u32x4_t*>(
+                reinterpret_cast<const uint32_t*>(rbase + (size_t)min(m, mrows - 1) * ld + aux_reg) + 32 * U + 8 * ql);
+            h = g[0];
+            l = g[1];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float a = x3_join(h[j >> 1], l[j >> 1], j & 1);
+            v[j] *= a > 0.f ? 1.0f : a + 1.0f;
+          }
+        }
+        u32x4_t h, l;
+        pn_split8(v, h, l);
+        *lh = h;
+        *ll = l;
+        if (save_reg >= 0 && m < mrows) {
+          u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(rbase + (size_t)m * ld + save_reg) + 32 * U +
+                                                  8 * ql);
+          g[0] = h;
+          g[1] = l;
+        }
+      }
+    }
+  };
+
+  // forward
+  for (int l = 0; l < pd.L; ++l) {
+    pn_zero(acc);
+    if (l == 0) {
+      const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnF[0], PN_H, L.INP);
+      pn_gemm<4, 4, 3>(acc, rw, 4 * wv, L.INP / 32, 0, 2 + nxk, 0, lane, il, ql,
+                       [&](int c) { return c < 2 ? act(c) : xsl(c - 2); });
+    } else {
+      const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnF[l], PN_H, PN_H);
+      pn_gemm<4, 4, 3>(acc, rw, 4 * wv, PN_HC, 0, PN_HC, 0, lane, il, ql, act);
+    }
+    pn_barrier();  // every wave's reads of the layer input are done
+    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], 0);
+    pn_barrier();
+  }
+  // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own granules)
+  {
+    pn_zero(acc);
+    const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnTF[pd.L], PN_H, 32 * nxk);
+    pn_gemm<4, 4, 3>(acc, rw, 4 * wv, nxk, 0, nxk, 0, lane, il, ql, xsl);
+    epilogue(PN_DELU_LDS, pd.nnTW[pd.L], nullptr, -1, 0);
+    // the forward's HBM stores of A_0 .. A_{L-1} complete (read back below: A_{l-1} by the lane that
+    // stored it, A_{L-1} by other waves for GX)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pn_barrier();
+  }
+  for (int l = pd.L - 1; l >= 1; --l) {
+    pn_zero(acc);
+    const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnTF[l], PN_H, PN_H);
+    pn_gemm<4, 4, 3>(acc, rw, 4 * wv, PN_HC, 0, PN_HC, 0, lane, il, ql, act);
+    pn_barrier();
+    epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, L.A[l - 1]);
+    pn_barrier();
+  }
+  // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act)
+  {
+    constexpr int UG = NB_GX == 2 ? 4 : 2;  // unit groups of 32 (NOP / 32)
+    const int ug = wv % UG, pg = wv / UG, p0 = 16 * NB_GX * pg;
+    constexpr int KG = 2 * PN_H;
+    pn_f4 ag[2][NB_GX];
+    pn_zero(ag);
+    const __amdgpu_buffer_rsrc_t rg = wsrc(pd.gxnoF, 32 * UG, KG);
+    pn_gemm<2, NB_GX, 3>(ag, rg, 2 * ug, KG / 32, 0, PN_HC, p0, lane, il, ql, act);
+    pn_barrier();
+    {
+      u32x4_t v[PN_HC];
+#pragma unroll
+      for (int c = 0; c < PN_HC; ++c) v[c] = *gsrc(L.A[pd.L - 1], c);
+#pragma unroll
+      for (int c = 0; c < PN_HC; ++c) *gdst(act(c)) = v[c];
+    }
+    pn_barrier();
+    pn_gemm<2, NB_GX, 3>(ag, rg, 2 * ug, KG / 32, PN_HC, PN_HC, p0, lane, il, ql, act);
+    const float* bias = pd.nnbP[pd.L];
+#pragma unroll
+    for (int b = 0; b < NB_GX; ++b) {
+      const int m = p0 + 16 * b + il;
+      if (m >= mrows) continue;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ag[0][b][r] * pd.gxnoW;
+        v[4 + r] = ag[1][b][r] * pd.gxnoW;
+      }
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * ug + 4 * ql);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * ug + 4 * ql + 16);
+      v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
+      v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+      x3_put8(rbase + (size_t)m * ld, L.GX, ug, ql, v);
+    }
+  }
+}
+
+}  // namespace dpi

@@ -153,3 +153,29 @@ def test_hjb_two_pipeline_chunks_equal_separate_calls():
     ev, eg = _rel(y[n - 1:n, :1], ref[:, :1]), _rel(y[n - 1:n, 1:], ref[:, 1:])
     print(f"point {n - 1} (second chunk): value {ev:.2e} grad {eg:.2e}")
     assert ev < TOL and eg < TOL, (ev, eg)
+
+
+@pytest.mark.parametrize("n,M", [(64, 4096), (3, 128)])
+def test_hjb_fused_chain_equals_layer_wise_chain(n, M, monkeypatch):
+    """k_pis_net (the VJP chain in one launch, activations in LDS) against the nine k_gemm_x3h
+    launches it replaces (DPI_PIS_FUSED=0): the same products in the same order, so the moments and
+    the labels are bitwise equal — at the configs[2] size (262,208 rows, 4,097 full 64-row tiles) and
+    at 387 rows (a partial last tile)."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(0)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=8, seed=5)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DPI_PIS_FUSED", fused)
+        ws = gen.point_baseline(tx)
+        mom = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
+        out[fused] = (mom, gen.finalize(mom, M, L.DPI_BOTH, ws))
+    assert torch.isfinite(out["1"][1]).all()
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])

@@ -623,12 +623,14 @@ def test_more_paths_than_one_call_takes(hessians):
     from deeppicarditeration_amd import _lib as L
     from oracle import dpi_oracle as O
     M, K = 2 * L.DPI_PATHS_PER_CALL_MAX, 4
+    # (the fp64 Hessian oracle over 131,072 paths: 4 dimensions and a 2 x 16 network keep it to seconds)
+    nx = 4 if hessians else 100
     if hessians:
-        eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
         torch.manual_seed(3)
-        net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
-        oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
-        act = ["ELU"] * 3
+        eq = dpi.GBMEquationComplexExact(nx, 1.0, 1.0, w=0.3 * torch.randn(2, nx + 1), v=torch.randn(2, 1))
+        net = dpi.construct_mlp(nx + 1, 1, [16] * 2, ["ELU"] * 2, None)
+        oeq = O.GBMEquationComplexExact(nx, eq.w.numpy(), eq.v.numpy())
+        act = ["ELU"] * 2
     else:
         eq = dpi.Cha(nx=100, T=1.0, k=5.0, alpha=1.0)
         torch.manual_seed(0)
@@ -647,10 +649,10 @@ def test_more_paths_than_one_call_takes(hessians):
            else O.labels_grad(oeq, onet, txh, M, K, 1, 1, 0, m_chunk=4096))
     def rel(a, b):
         return float(np.linalg.norm(a - b) / np.linalg.norm(b))
-    ev, eg = rel(y[:, :1], ref[:, :1]), rel(y[:, 1:101], ref[:, 1:101])
+    ev, eg = rel(y[:, :1], ref[:, :1]), rel(y[:, 1:nx + 1], ref[:, 1:nx + 1])
     print(f"M = {M}: value {ev:.2e} grad {eg:.2e}")
     assert ev < 1e-4 and eg < 1e-4
     if hessians:
-        eh = rel(y[:, 101:], ref[:, 101:])
+        eh = rel(y[:, nx + 1:], ref[:, nx + 1:])
         print(f"hessian {eh:.2e}")
         assert eh < 1e-4
