@@ -51,8 +51,9 @@ WORKLOADS = {
                               "in total, MC-sharded 4096/N paths per GPU, K=50 EM steps, MLP 101-128x4-1 ELU, one RCCL "
                               "all-gather of label moments + canonical tree reduce (BASELINE configs[3])"),
     "hjb": dict(cfg="configs[2]", eq="OUProcessEquation", widths=[512] * 4, pis=True, points=64, m_per_gpu=4096, K=50,
-                sdgd=0, flop=3.73e6, peak="split", kernel="k_pis_rollout + k_gemm_x3 chain (fp16-split) + "
-                                                           "k_pis_final + k_reduce per dpi_label_moments call",
+                sdgd=0, flop=3.73e6, peak="split", kernel="k_pis_rollout + k_pis_time + k_pis_net (the fp16-split "
+                                                           "nn_module VJP chain in one launch) + k_pis_final + "
+                                                           "k_reduce per dpi_label_moments call",
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
                      "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
     "gbm_hess": dict(cfg="configs[4] stretch (Malliavin Hessian labels)", eq="GBMEquationComplexExact", widths=[64] * 3,
@@ -83,8 +84,8 @@ def parse():
     ap.add_argument("--pipelined", action="store_true", help="two-phase labels also at N = 1 (default: N > 1 only)")
     ap.add_argument("--prepare", action="store_true", help="two-phase labels with the next batch's sampling and "
                                                            "baseline on a low-priority side stream, the path "
-                                                           "kernels on a high-priority stream (default for hjb)")
-    ap.add_argument("--no-prepare", action="store_true", help="hjb: one stream")
+                                                           "kernels on a high-priority stream")
+    ap.add_argument("--no-prepare", action="store_true", help="one stream (the default; overrides --prepare)")
     return ap.parse_args()
 
 
@@ -220,7 +221,9 @@ def main():
     # the fused-kernel workloads, whose one path launch the side work would slow.
     if args.workload is None:
         args.workload = "burgers" if world == 1 else "burgers_cfg3"
-    args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis"))) and not args.no_prepare
+    # (hjb ran prepared by default while its chain was nine GEMM launches whose blocks left room for the
+    # next batch's rollout; k_pis_net holds a CU's whole LDS, so one stream is now as fast: DESIGN §2.4)
+    args.prepare = args.prepare and not args.no_prepare
     if args.prepare:
         lo, hi = torch.cuda.Stream.priority_range()
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=hi))

@@ -1005,10 +1005,19 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   // the VJP chain as one launch with the activations in LDS (dpi_pisnet.h), where the shape fits
   if (vjp && R > 0 && pis_fused_on() && pis_fused_fits(pd, L)) {
     const dim3 grid((R + PN_BM - 1) / PN_BM), block(PN_THREADS);
-    if (NOP == 128)
-      hipLaunchKernelGGL(k_pis_net<2>, grid, block, 0, st, pd, rows, L, R);
-    else
-      hipLaunchKernelGGL(k_pis_net<1>, grid, block, 0, st, pd, rows, L, R);
+    const char* e = std::getenv("DPI_PIS_NT");
+    const bool nts = !e || std::atoi(e) != 0;
+    if (NOP == 128) {
+      if (nts)
+        hipLaunchKernelGGL((k_pis_net<2, true>), grid, block, 0, st, pd, rows, L, R);
+      else
+        hipLaunchKernelGGL((k_pis_net<2, false>), grid, block, 0, st, pd, rows, L, R);
+    } else {
+      if (nts)
+        hipLaunchKernelGGL((k_pis_net<1, true>), grid, block, 0, st, pd, rows, L, R);
+      else
+        hipLaunchKernelGGL((k_pis_net<1, false>), grid, block, 0, st, pd, rows, L, R);
+    }
     return L;
   }
   int Kp = L.INP;

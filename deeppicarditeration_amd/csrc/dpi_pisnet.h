@@ -69,30 +69,42 @@ __device__ __forceinline__ void pn_split8(const float (&v)[8], u32x4_t& h, u32x4
   }
 }
 
-// acc[t][b] += sum over chunks c < nk of W[tile T0 + t][chunk c0 + c] . slab(c)[rows p0 + 16 b + il]
-// W: a fragment-major matrix (NetPisDev::nnF, pack_frag_major) with nkw chunks per row, behind the
-// buffer resource rw; every weight load is lane l's 16 B of a 1 KB block (one VGPR offset for all;
-// tile, chunk and hi / lo in the scalar offset).  The weights run NS - 1 chunks ahead in NS
-// register sets (the loop unrolled by NS, branch-free: loads past the last chunk repeat it), so a
-// load has NS - 1 chunks of MFMAs to arrive from L2; the B fragments (LDS) are read per chunk just
+// Weight fragment register sets of pn_gemm (NT <= 4 unit tiles): three, rotating.
+struct PnW {
+  pn_h8 ah[3][4], al[3][4];
+};
+// set S <- chunk c of tiles T0 .. T0 + NT - 1 of a fragment-major matrix (pack_frag_major) with nkw
+// chunks per row behind rw: lane l's 16 B of each 1 KB block (one VGPR offset for every load; tile,
+// chunk and hi / lo ride in the scalar offset)
+template <int NT, int S>
+__device__ __forceinline__ void pn_ldw(PnW& w, __amdgpu_buffer_rsrc_t rw, int vo, int T0, int nkw, int c) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int so = ((T0 + t) * nkw + c) * 2048;
+    w.ah[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so, 0));
+    w.al[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so + 1024, 0));
+  }
+}
+// a product's first two chunks into sets 0 and 1 — issued ahead of pn_gemm, under the previous
+// product's epilogue and barriers
+template <int NT>
+__device__ __forceinline__ void pn_pre(PnW& w, __amdgpu_buffer_rsrc_t rw, int vo, int T0, int nkw, int c0, int nk) {
+  pn_ldw<NT, 0>(w, rw, vo, T0, nkw, c0);
+  pn_ldw<NT, 1>(w, rw, vo, T0, nkw, c0 + min(1, nk - 1));
+}
+
+// acc[t][b] += sum over chunks c < nk of W[tile T0 + t][chunk c0 + c] . slab(c)[rows p0 + 16 b + il],
+// sets 0 and 1 already holding chunks c0, c0 + 1 (pn_pre).  The weights run two chunks ahead in
+// the three sets (the loop unrolled by three, branch-free: loads past the last chunk repeat it), so
+// a load has two chunks of MFMAs to arrive from L2; the B fragments (LDS) are read per chunk just
 // before its MFMAs.  Rows p0 + 16 b + il share x3_swz, so two LDS addresses serve every path tile.
-template <int NT, int NB, int NS, class Slab>
-__device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], __amdgpu_buffer_rsrc_t rw, int T0, int nkw, int c0, int nk,
-                                        int p0, int lane, int il, int ql, Slab slab) {
-  pn_h8 ah[NS][NT], al[NS][NT];
-  const int vo = 16 * lane;
+// Per output the products of k_gemm_x3h in its order: hi.hi, hi.lo, lo.hi per chunk.
+template <int NT, int NB, class Slab>
+__device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], PnW& w, __amdgpu_buffer_rsrc_t rw, int vo, int T0, int nkw,
+                                        int c0, int nk, int p0, int il, int ql, Slab slab) {
   const int sw = x3_swz(il);  // = x3_swz(p0 + 16 b + il): p0 % 16 == 0
   const int oh = (p0 + il) * 32 + 4 * ((2 * ql) ^ sw), ol = (p0 + il) * 32 + 4 * ((2 * ql + 1) ^ sw);
-  auto ldw = [&](int c, auto Sc) {
-    constexpr int S = decltype(Sc)::value;
-    c = min(c, nk - 1);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int so = ((T0 + t) * nkw + c0 + c) * 2048;
-      ah[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so, 0));
-      al[S][t] = __builtin_bit_cast(pn_h8, __builtin_amdgcn_raw_buffer_load_b128(rw, vo, so + 1024, 0));
-    }
-  };
+  auto ldw = [&](int c, auto Sc) { pn_ldw<NT, decltype(Sc)::value>(w, rw, vo, T0, nkw, c0 + min(c, nk - 1)); };
   auto mm = [&](int c, auto Sc) {
     constexpr int S = decltype(Sc)::value;
     const uint32_t* s = slab(c);
@@ -106,19 +118,16 @@ __device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], __amdgpu_buffer_rs
     for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[S][t], bh[b], acc[t][b], 0, 0, 0);
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[S][t], bl[b], acc[t][b], 0, 0, 0);
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[S][t], bh[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bh[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bl[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.al[S][t], bh[b], acc[t][b], 0, 0, 0);
       }
   };
-  static_assert(NS == 3, "the rotation below is written for three sets");
   constexpr std::integral_constant<int, 0> I0{};
   constexpr std::integral_constant<int, 1> I1{};
   constexpr std::integral_constant<int, 2> I2{};
   // sched_barrier(0): the scheduler keeps each load group where it is written (left alone it sinks
   // every load next to its first use to shorten live ranges)
-  ldw(0, I0);
-  ldw(1, I1);
   int c = 0;
 #pragma unroll 1
   for (; c + 3 <= nk; c += 3) {
@@ -137,6 +146,7 @@ __device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], __amdgpu_buffer_rs
   }
   if (c < nk) mm(c, I0);
   if (c + 1 < nk) mm(c + 1, I1);
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int NT, int NB>
@@ -149,9 +159,24 @@ __device__ __forceinline__ void pn_zero(pn_f4 (&acc)[NT][NB]) {
 
 enum { PN_ELU = 0, PN_DELU_LDS = 1, PN_DELU_HBM = 2 };
 
+// row traffic (IN, the saved activations, GX) with the non-temporal hint when NTS, so the streams
+// through L2 do not evict the chain's weights (7 MB, shared by every block of the XCD)
+template <bool NTS>
+__device__ __forceinline__ u32x4_t pn_ld(const u32x4_t* p) {
+  if constexpr (NTS) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NTS>
+__device__ __forceinline__ void pn_st(u32x4_t* p, u32x4_t v) {
+  if constexpr (NTS)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 // NB_GX: path tiles per wave of the GX product (NOP = 128: 4 unit groups of 32 x 2 path groups;
 // NOP = 64: 2 x 4).  R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.
-template <int NB_GX>
+template <int NB_GX, bool NTS>
 __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* __restrict__ rows, PisRows L, int R) {
   __shared__ PnLds lds;
   const int tid = threadIdx.x, lane = tid & 63, il = lane & 15, ql = lane >> 4;
@@ -178,7 +203,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     u32x4_t v[2 + PN_XC];
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
-      if (c < 2 + nxk) v[c] = *gsrc(L.IN, c);
+      if (c < 2 + nxk) v[c] = pn_ld<NTS>(gsrc(L.IN, c));
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
       if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
@@ -187,20 +212,46 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
 
   // the 512-wide products: wave wv owns units 64 wv .. 64 wv + 63 (4 unit tiles) of all 64 rows
   pn_f4 acc[4][4];
-  // a fragment-major weight matrix of `rows` rows and Kp words per row
+  PnW w;
+  const int vo = 16 * lane;
+  // a fragment-major weight matrix of `rows_` rows and Kp words per row
   auto wsrc = [&](const uint32_t* W, int rows_, int Kp) { return pn_rsrc(W, (size_t)rows_ * Kp * 4); };
-  // epilogue of a 512-wide product: lane (il, ql) of path tile b holds units 64 wv + 16 t + 4 ql + r
-  // of row 16 b + il; unit tiles (2 c, 2 c + 1) form granule pair ql of chunk U = 2 wv + c
-  auto epilogue = [&](int kind, float ws, const float* bias, int save_reg, int aux_reg) {
+  constexpr int UG = NB_GX == 2 ? 4 : 2;  // GX unit groups of 32 (NOP / 32)
+  constexpr int KG = 2 * PN_H;             // GX's K: [D_0 | A_{L-1}]
+  const int ug = wv % UG, pg = wv / UG, p0g = 16 * NB_GX * pg;
+  const __amdgpu_buffer_rsrc_t rg = wsrc(pd.gxnoF, 32 * UG, KG);
+  // the next product's first two weight chunks, issued before the current epilogue
+  auto pre_fwd = [&](int l) {
+    if (l == 0)
+      pn_pre<4>(w, wsrc(pd.nnF[0], PN_H, L.INP), vo, 4 * wv, L.INP / 32, 0, 2 + nxk);
+    else
+      pn_pre<4>(w, wsrc(pd.nnF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC);
+  };
+  auto pre_vjp = [&](int l) {  // D_{l-1} = (nnT[l] D_l) * elu'(A_{l-1}); l == L: from X
+    if (l == pd.L)
+      pn_pre<4>(w, wsrc(pd.nnTF[l], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk);
+    else
+      pn_pre<4>(w, wsrc(pd.nnTF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC);
+  };
+  auto pre_gx = [&](int c0) { pn_pre<2>(w, rg, vo, 2 * ug, KG / 32, c0, PN_HC); };
+
+  // epilogue of a 512-wide product, in two halves: values -> split words in registers (and the HBM
+  // copy) before the barrier that releases the layer input, the LDS stores after it.  Lane (il, ql)
+  // of path tile b holds units 64 wv + 16 t + 4 ql + r of row 16 b + il; unit tiles (2 c, 2 c + 1)
+  // form granule pair ql of chunk U = 2 wv + c.
+  u32x4_t eh[4][2], el[4][2];
+  auto lds_at = [&](int b, int c, int hl) {
+    const int m = 16 * b + il;
+    return reinterpret_cast<u32x4_t*>(act(2 * wv + c) + m * 32 + 4 * ((2 * ql + hl) ^ x3_swz(m)));
+  };
+  auto epi_values = [&](int kind, float ws, const float* bias, int save_reg, const u32x4_t (&xh)[4][2],
+                        const u32x4_t (&xl)[4][2]) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int m = 16 * b + il;
-      const int s = x3_swz(m);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int U = 2 * wv + c;
-        u32x4_t* lh = reinterpret_cast<u32x4_t*>(act(U) + m * 32 + 4 * ((2 * ql) ^ s));
-        u32x4_t* ll = reinterpret_cast<u32x4_t*>(act(U) + m * 32 + 4 * ((2 * ql + 1) ^ s));
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -215,93 +266,130 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
         } else {
-          u32x4_t h, l;
-          if (kind == PN_DELU_LDS) {  // elu' of A_{L-1}, still in this wave's own granules
-            h = *lh;
-            l = *ll;
-          } else {
-            const u32x4_t* g = reinterpret_cast<const u32x4_t*>(
-                reinterpret_cast<const uint32_t*>(rbase + (size_t)min(m, mrows - 1) * ld + aux_reg) + 32 * U + 8 * ql);
-            h = g[0];
-            l = g[1];
-          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float a = x3_join(h[j >> 1], l[j >> 1], j & 1);
+            const float a = x3_join(xh[b][c][j >> 1], xl[b][c][j >> 1], j & 1);
             v[j] *= a > 0.f ? 1.0f : a + 1.0f;
           }
         }
-        u32x4_t h, l;
-        pn_split8(v, h, l);
-        *lh = h;
-        *ll = l;
+        pn_split8(v, eh[b][c], el[b][c]);
         if (save_reg >= 0 && m < mrows) {
           u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(rbase + (size_t)m * ld + save_reg) + 32 * U +
                                                   8 * ql);
-          g[0] = h;
-          g[1] = l;
+          pn_st<NTS>(g, eh[b][c]);
+          pn_st<NTS>(g + 1, el[b][c]);
         }
       }
     }
   };
+  auto epi_store = [&]() {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        *lds_at(b, c, 0) = eh[b][c];
+        *lds_at(b, c, 1) = el[b][c];
+      }
+  };
+  u32x4_t xh[4][2], xl[4][2];  // elu' operands of the VJP epilogues
+
+  pre_fwd(0);
+  // IN: the time embedding (chunks 0, 1) -> act, X (chunks 2 ..) -> xs
+  {
+    u32x4_t v[2 + PN_XC];
+#pragma unroll
+    for (int c = 0; c < 2 + PN_XC; ++c)
+      if (c < 2 + nxk) v[c] = pn_ld<NTS>(gsrc(L.IN, c));
+#pragma unroll
+    for (int c = 0; c < 2 + PN_XC; ++c)
+      if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
+  }
+  pn_barrier();
 
   // forward
   for (int l = 0; l < pd.L; ++l) {
     pn_zero(acc);
-    if (l == 0) {
-      const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnF[0], PN_H, L.INP);
-      pn_gemm<4, 4, 3>(acc, rw, 4 * wv, L.INP / 32, 0, 2 + nxk, 0, lane, il, ql,
-                       [&](int c) { return c < 2 ? act(c) : xsl(c - 2); });
-    } else {
-      const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnF[l], PN_H, PN_H);
-      pn_gemm<4, 4, 3>(acc, rw, 4 * wv, PN_HC, 0, PN_HC, 0, lane, il, ql, act);
-    }
+    if (l == 0)
+      pn_gemm<4, 4>(acc, w, wsrc(pd.nnF[0], PN_H, L.INP), vo, 4 * wv, L.INP / 32, 0, 2 + nxk, 0, il, ql,
+                    [&](int c) { return c < 2 ? act(c) : xsl(c - 2); });
+    else
+      pn_gemm<4, 4>(acc, w, wsrc(pd.nnF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC, 0, il, ql, act);
+    if (l + 1 < pd.L)
+      pre_fwd(l + 1);
+    else
+      pre_vjp(pd.L);
+    epi_values(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], xh, xl);
     pn_barrier();  // every wave's reads of the layer input are done
-    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], 0);
+    epi_store();
     pn_barrier();
   }
-  // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own granules)
+  // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
+  // granules, so no barrier before the stores)
   {
     pn_zero(acc);
-    const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnTF[pd.L], PN_H, 32 * nxk);
-    pn_gemm<4, 4, 3>(acc, rw, 4 * wv, nxk, 0, nxk, 0, lane, il, ql, xsl);
-    epilogue(PN_DELU_LDS, pd.nnTW[pd.L], nullptr, -1, 0);
+    pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[pd.L], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk, 0, il, ql, xsl);
     // the forward's HBM stores of A_0 .. A_{L-1} complete (read back below: A_{l-1} by the lane that
     // stored it, A_{L-1} by other waves for GX)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        xh[b][c] = *lds_at(b, c, 0);
+        xl[b][c] = *lds_at(b, c, 1);
+      }
+    if (pd.L > 1)
+      pre_vjp(pd.L - 1);
+    else
+      pre_gx(0);
+    epi_values(PN_DELU_LDS, pd.nnTW[pd.L], nullptr, -1, xh, xl);
+    epi_store();
     pn_barrier();
   }
   for (int l = pd.L - 1; l >= 1; --l) {
     pn_zero(acc);
-    const __amdgpu_buffer_rsrc_t rw = wsrc(pd.nnTF[l], PN_H, PN_H);
-    pn_gemm<4, 4, 3>(acc, rw, 4 * wv, PN_HC, 0, PN_HC, 0, lane, il, ql, act);
+    pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC, 0, il, ql, act);
+    // elu'(A_{l-1}): this lane's own HBM copy, issued before the next weights so the counted wait
+    // for it leaves those in flight
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const u32x4_t* g = reinterpret_cast<const u32x4_t*>(
+            reinterpret_cast<const uint32_t*>(rbase + (size_t)min(16 * b + il, mrows - 1) * ld + L.A[l - 1]) +
+            32 * (2 * wv + c) + 8 * ql);
+        xh[b][c] = pn_ld<NTS>(g);
+        xl[b][c] = pn_ld<NTS>(g + 1);
+      }
+    if (l > 1)
+      pre_vjp(l - 1);
+    else
+      pre_gx(0);
+    epi_values(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, xh, xl);
     pn_barrier();
-    epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, L.A[l - 1]);
+    epi_store();
     pn_barrier();
   }
   // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act)
   {
-    constexpr int UG = NB_GX == 2 ? 4 : 2;  // unit groups of 32 (NOP / 32)
-    const int ug = wv % UG, pg = wv / UG, p0 = 16 * NB_GX * pg;
-    constexpr int KG = 2 * PN_H;
     pn_f4 ag[2][NB_GX];
     pn_zero(ag);
-    const __amdgpu_buffer_rsrc_t rg = wsrc(pd.gxnoF, 32 * UG, KG);
-    pn_gemm<2, NB_GX, 3>(ag, rg, 2 * ug, KG / 32, 0, PN_HC, p0, lane, il, ql, act);
-    pn_barrier();
+    pn_gemm<2, NB_GX>(ag, w, rg, vo, 2 * ug, KG / 32, 0, PN_HC, p0g, il, ql, act);
+    pre_gx(PN_HC);
     {
       u32x4_t v[PN_HC];
 #pragma unroll
-      for (int c = 0; c < PN_HC; ++c) v[c] = *gsrc(L.A[pd.L - 1], c);
+      for (int c = 0; c < PN_HC; ++c) v[c] = pn_ld<NTS>(gsrc(L.A[pd.L - 1], c));
+      pn_barrier();
 #pragma unroll
       for (int c = 0; c < PN_HC; ++c) *gdst(act(c)) = v[c];
     }
     pn_barrier();
-    pn_gemm<2, NB_GX, 3>(ag, rg, 2 * ug, KG / 32, PN_HC, PN_HC, p0, lane, il, ql, act);
+    pn_gemm<2, NB_GX>(ag, w, rg, vo, 2 * ug, KG / 32, PN_HC, PN_HC, p0g, il, ql, act);
     const float* bias = pd.nnbP[pd.L];
 #pragma unroll
     for (int b = 0; b < NB_GX; ++b) {
-      const int m = p0 + 16 * b + il;
+      const int m = p0g + 16 * b + il;
       if (m >= mrows) continue;
       float v[8];
 #pragma unroll
