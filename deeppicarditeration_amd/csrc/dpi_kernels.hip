@@ -1006,18 +1006,10 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   if (vjp && R > 0 && pis_fused_on() && pis_fused_fits(pd, L)) {
     const dim3 grid((R + PN_BM - 1) / PN_BM), block(PN_THREADS);
     const char* e = std::getenv("DPI_PIS_NT");
-    const bool nts = !e || std::atoi(e) != 0;
-    if (NOP == 128) {
-      if (nts)
-        hipLaunchKernelGGL((k_pis_net<2, true>), grid, block, 0, st, pd, rows, L, R);
-      else
-        hipLaunchKernelGGL((k_pis_net<2, false>), grid, block, 0, st, pd, rows, L, R);
-    } else {
-      if (nts)
-        hipLaunchKernelGGL((k_pis_net<1, true>), grid, block, 0, st, pd, rows, L, R);
-      else
-        hipLaunchKernelGGL((k_pis_net<1, false>), grid, block, 0, st, pd, rows, L, R);
-    }
+    if (!e || std::atoi(e) != 0)
+      hipLaunchKernelGGL(k_pis_net<true>, grid, block, 0, st, pd, rows, L, R);
+    else
+      hipLaunchKernelGGL(k_pis_net<false>, grid, block, 0, st, pd, rows, L, R);
     return L;
   }
   int Kp = L.INP;

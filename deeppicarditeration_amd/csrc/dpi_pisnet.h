@@ -174,9 +174,9 @@ __device__ __forceinline__ void pn_st(u32x4_t* p, u32x4_t v) {
     *p = v;
 }
 
-// NB_GX: path tiles per wave of the GX product (NOP = 128: 4 unit groups of 32 x 2 path groups;
-// NOP = 64: 2 x 4).  R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.
-template <int NB_GX, bool NTS>
+// R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.  NTS: the non-temporal hint on
+// the row traffic (DPI_PIS_NT, default on).
+template <bool NTS>
 __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* __restrict__ rows, PisRows L, int R) {
   __shared__ PnLds lds;
   const int tid = threadIdx.x, lane = tid & 63, il = lane & 15, ql = lane >> 4;
@@ -216,10 +216,9 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
   const int vo = 16 * lane;
   // a fragment-major weight matrix of `rows_` rows and Kp words per row
   auto wsrc = [&](const uint32_t* W, int rows_, int Kp) { return pn_rsrc(W, (size_t)rows_ * Kp * 4); };
-  constexpr int UG = NB_GX == 2 ? 4 : 2;  // GX unit groups of 32 (NOP / 32)
-  constexpr int KG = 2 * PN_H;             // GX's K: [D_0 | A_{L-1}]
-  const int ug = wv % UG, pg = wv / UG, p0g = 16 * NB_GX * pg;
-  const __amdgpu_buffer_rsrc_t rg = wsrc(pd.gxnoF, 32 * UG, KG);
+  constexpr int KG = 2 * PN_H;                  // GX's K: [D_0 | A_{L-1}]
+  const int nopt = ((pd.nx + 63) & ~63) / 16;  // GX unit tiles (4 or 8)
+  const __amdgpu_buffer_rsrc_t rg = wsrc(pd.gxnoF, 16 * nopt, KG);
   // the next product's first two weight chunks, issued before the current epilogue
   auto pre_fwd = [&](int l) {
     if (l == 0)
@@ -233,7 +232,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     else
       pn_pre<4>(w, wsrc(pd.nnTF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC);
   };
-  auto pre_gx = [&](int c0) { pn_pre<2>(w, rg, vo, 2 * ug, KG / 32, c0, PN_HC); };
+  auto pre_gx = [&](int c0) { pn_pre<1>(w, rg, vo, min(wv, nopt - 1), KG / 32, c0, PN_HC); };
 
   // epilogue of a 512-wide product, in two halves: values -> split words in registers (and the HBM
   // copy) before the barrier that releases the layer input, the LDS stores after it.  Lane (il, ql)
@@ -370,11 +369,14 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     epi_store();
     pn_barrier();
   }
-  // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act)
+  // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act).
+  // Wave wv < nopt takes unit tile wv for all 64 rows, so each weight fragment is read once per
+  // block; the two tiles of a granule pair then meet in the X image (free since D_{L-1}) as fp32.
   {
-    pn_f4 ag[2][NB_GX];
+    pn_f4 ag[1][4];
     pn_zero(ag);
-    pn_gemm<2, NB_GX>(ag, w, rg, vo, 2 * ug, KG / 32, 0, PN_HC, p0g, il, ql, act);
+    const bool live = wv < nopt;
+    if (live) pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, 0, PN_HC, 0, il, ql, act);
     pre_gx(PN_HC);
     {
       u32x4_t v[PN_HC];
@@ -385,23 +387,29 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
       for (int c = 0; c < PN_HC; ++c) *gdst(act(c)) = v[c];
     }
     pn_barrier();
-    pn_gemm<2, NB_GX>(ag, w, rg, vo, 2 * ug, KG / 32, PN_HC, PN_HC, p0g, il, ql, act);
-    const float* bias = pd.nnbP[pd.L];
+    float* gx = reinterpret_cast<float*>(lds.xs);  // row m: 128 fp32
+    if (live) {
+      pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, PN_HC, PN_HC, 0, il, ql, act);
+      const float* bias = pd.nnbP[pd.L] + 16 * wv + 4 * ql;
 #pragma unroll
-    for (int b = 0; b < NB_GX; ++b) {
-      const int m = p0g + 16 * b + il;
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = ag[0][b][r] * pd.gxnoW;  // k_gemm_x3h's EPI_BIAS arithmetic
+          v += bias[r];
+          gx[(16 * b + il) * 128 + 16 * wv + 4 * ql + r] = v;
+        }
+    }
+    pn_barrier();
+    // row m, chunk U, granule pair q: units 32 U + 4 q + (j & 3) + 16 (j >> 2)
+    const int nu = nopt / 2;
+    for (int i = tid; i < PN_BM * nu * 4; i += PN_THREADS) {
+      const int q = i & 3, U = (i >> 2) % nu, m = (i >> 2) / nu;
       if (m >= mrows) continue;
       float v[8];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = ag[0][b][r] * pd.gxnoW;
-        v[4 + r] = ag[1][b][r] * pd.gxnoW;
-      }
-      const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * ug + 4 * ql);
-      const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * ug + 4 * ql + 16);
-      v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
-      v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
-      x3_put8(rbase + (size_t)m * ld, L.GX, ug, ql, v);
+      for (int j = 0; j < 8; ++j) v[j] = gx[m * 128 + 32 * U + 4 * q + (j & 3) + 16 * (j >> 2)];
+      x3_put8(rbase + (size_t)m * ld, L.GX, U, q, v);
     }
   }
 }
