@@ -1301,137 +1301,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
 }
 
-// The same per-point baseline for the MLP of a first-order equation (not GBM) with 4 waves and
-// one barrier per layer instead of k_baseline's 16 waves and two barriers + a slice combine per
-// mat-vec (16 us per Burgers label call, 4 % of the step, serialised before k_paths).  Mat-vec
-// y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H)): wave w owns units 32w .. 32w + 31, lane l unit
-// 32w + l % 32 over the k-half l / 32 (the two halves' rows of Wt are 128 contiguous bytes per k),
-// the halves joined by one cross-lane swap; the layer input comes from a double-buffered LDS vector
-// (broadcast reads), so a layer's only barrier publishes its output.  Every weight load of a layer
-// is issued before its first FMA.  Same formulas as k_baseline (g(x), bx = b1 + W1x x, f_b at
-// (t, x, u, grad u)); the sums run in another fixed order, so bx and f_b agree with k_baseline to
-// fp32 rounding.
-constexpr int NTHB4 = 256;
-template <int KIND>
-__global__ __launch_bounds__(NTHB4) void k_baseline_w4(EqDev e, NetDev net, const float* __restrict__ tx, int n,
-                                                       float* __restrict__ gx, float* __restrict__ fb,
-                                                       float* __restrict__ bx) {
-  static_assert(KIND != DPI_EQ_GBM, "GBM's baseline carries the Hessian diagonal: k_baseline");
-  __shared__ __attribute__((aligned(16))) float xs[NXP_MAX];
-  __shared__ __attribute__((aligned(16))) float vb[2][HMAX];   // layer input / output, double-buffered
-  __shared__ float act[4][HMAX];                                // activations (elu' of the backward pass)
-  __shared__ float red[NTHB4 / 64][NSG];
-  const int i = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int nx = e.nx, F = 1 + nx, H = net.H, L = net.L, nxp = net.nxp;
-  const float* row = tx + (size_t)i * F;
-  const float t = row[0];
-  for (int d = tid; d < NXP_MAX; d += NTHB4) xs[d] = d < nx ? row[1 + d] : 0.f;
-  for (int k = tid; k < 2 * HMAX; k += NTHB4) (&vb[0][0])[k] = 0.f;  // the upper half-K reads of H < 64
-  const int h = 32 * wv + (lane & 31), kh = lane >> 5;
-  const bool own = h < H;  // H <= 128: units 0 .. H-1
-  // y = sum over this lane's k-half of Wt[k][h] v[k]; both halves end with the full sum
-  auto matvec = [&](const float* __restrict__ Wt, int ldw, const float* v, int K) -> float {
-    const int kc = ((K + 63) >> 6) << 5, k0 = kh * kc;  // half of K rounded up to 32
-    float w[64];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) w[j] = (own && j < kc && k0 + j < K) ? Wt[(size_t)(k0 + j) * ldw + h] : 0.f;
-    float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-    for (int j = 0; j < 64; j += 4) {
-      if (j < kc) {
-        const float4 x = *reinterpret_cast<const float4*>(v + k0 + j);  // LDS broadcast
-        a0 = fmaf(w[j], x.x, a0);
-        a1 = fmaf(w[j + 1], x.y, a1);
-        a0 = fmaf(w[j + 2], x.z, a0);
-        a1 = fmaf(w[j + 3], x.w, a1);
-      }
-    }
-    const float s = a0 + a1;
-    const float o = __shfl_xor(s, 32, 64);
-    return kh ? o + s : s + o;  // (half 0) + (half 1) on both lanes
-  };
-  // block sum of NSG values per thread in fixed order (wave butterflies, then waves 0..3)
-  auto block_sums = [&](float (&st)[NSG]) {
-#pragma unroll
-    for (int c = 0; c < NSG; ++c) st[c] = wave_sum(st[c]);
-    if (lane == 0)
-#pragma unroll
-      for (int c = 0; c < NSG; ++c) red[wv][c] = st[c];
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < NSG; ++c) st[c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
-    __syncthreads();  // red reusable
-  };
-  __syncthreads();  // xs
-  {  // g(x)
-    float st[NSG];
-#pragma unroll
-    for (int c = 0; c < NSG; ++c) st[c] = 0.f;
-    for (int d = tid; d < nx; d += NTHB4) Eq<KIND>::gstat(e, d, xs[d], st);
-    block_sums(st);
-    if (tid == 0) gx[i] = Eq<KIND>::gfin(e, st);
-  }
-  // layer 1 (K = nxp, padded x entries are 0)
-  {
-    const float acc = matvec(net.W1xT, H, xs, nxp);
-    if (own && kh == 0) {
-      bx[(size_t)i * H + h] = net.b1[h] + acc;
-      const float a = elu(fmaf(net.w1t[h], t, net.b1[h] + acc));
-      act[0][h] = a;
-      vb[0][h] = a;
-    }
-    __syncthreads();
-  }
-  int cur = 0;
-  for (int l = 1; l < L; ++l) {
-    const float acc = matvec(net.WT[l], H, vb[cur], H);
-    if (own && kh == 0) {
-      const float a = elu(acc + net.b[l][h]);
-      act[l][h] = a;
-      vb[cur ^ 1][h] = a;
-    }
-    cur ^= 1;
-    __syncthreads();
-  }
-  float st[NSG];
-#pragma unroll
-  for (int c = 0; c < NSG; ++c) st[c] = 0.f;
-  st[0] = (own && kh == 0) ? net.wout[h] * act[L - 1][h] : 0.f;
-  // the first adjoint vector (its own buffer write precedes block_sums' barrier)
-  if (own && kh == 0) vb[cur ^ 1][h] = net.wout[h] * delu_from_a(act[L - 1][h]);
-  cur ^= 1;
-  block_sums(st);
-  const float u = st[0] + net.bout;
-  for (int l = L - 2; l >= 0; --l) {
-    // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
-    const float acc = matvec(net.W[l + 1], H, vb[cur], H);
-    if (own && kh == 0) vb[cur ^ 1][h] = acc * delu_from_a(act[l][h]);
-    cur ^= 1;
-    __syncthreads();
-  }
-  float gs = 0.f, gA = 0.f, gB = 0.f;
-#pragma unroll
-  for (int c = 0; c < NSG; ++c) st[c] = 0.f;
-  if (!Eq<KIND>::GRAD_FULL) {
-    st[0] = (own && kh == 0) ? net.c1[h] * vb[cur][h] : 0.f;
-    block_sums(st);
-    gs = st[0];
-  } else {
-    float A = 0.f, B = 0.f;
-    for (int d = tid; d < nx; d += NTHB4) {
-      float z = 0.f;
-      for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], vb[cur][k], z);
-      Eq<KIND>::gacc(e, d, xs[d], z, A, B);
-    }
-    st[0] = A;
-    st[1] = B;
-    block_sums(st);
-    gA = st[0];
-    gB = st[1];
-  }
-  if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
-}
-
 struct PathArgs {
   const float* tx;
   const float* gx;

@@ -36,13 +36,6 @@ struct Launch {
   bool td = false;    // k_paths with the TD estimators (problem td_dt > 0)
 };
 
-// The 4-wave per-point baseline (k_baseline_w4) for first-order MLP problems; DPI_BASELINE_W4=0
-// selects the 16-wave k_baseline (ablation; read per call).
-inline bool baseline_w4_on() {
-  const char* e = std::getenv("DPI_BASELINE_W4");
-  return !e || std::atoi(e) != 0;
-}
-
 // TDV: the TD-estimator k_paths variants, compiled in translation units of their own
 // (dpi_paths_td_*.hip): sharing a unit with the plain kernels perturbs the register allocation
 // of the plain fused-MLP kernel (6 spills at 256 VGPRs instead of none at 252).
@@ -60,17 +53,9 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
       hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
                          net->d, *q.a);
     }
-  } else if (q.baseline) {
-    if constexpr (KIND != DPI_EQ_GBM && !Z) {
-      if (baseline_w4_on()) {
-        hipLaunchKernelGGL((k_baseline_w4<KIND>), dim3(q.n), dim3(NTHB4), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
-                           q.bx);
-        return;
-      }
-    }
+  } else if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                        q.bx, q.hb);
-  }
   else if (q.hess) {
     if constexpr (KIND == DPI_EQ_GBM) {
       EqDev e2 = p->e;

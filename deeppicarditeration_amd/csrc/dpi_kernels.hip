@@ -1189,49 +1189,6 @@ static int pis_prep_per_cu() {
   return v;
 }
 
-// The n per-point baseline rows as their own chain on one CU, beside the rollout (DPI_PIS_BASE_SIDE,
-// default on).  In the path chunk's k_pis_net launch they were the 4,097th 64-row tile: a 17th
-// round on one CU for 64 rows (k_pis_net is bound by its weight feed, so a tile costs the same
-// whatever its rows).  Here the rollout runs on a stream masked to every CU but BASE_CUS, the
-// baseline chain (k_pis_points, k_pis_time, k_pis_net over the n rows, then k_pis_base_final's
-// f_b) on a stream masked to BASE_CUS, both after an event on the caller's stream; the caller's
-// stream waits for the rollout before the path chain and for f_b before k_pis_final.  Row results
-// do not depend on which launch carries the row, so the labels are bitwise those of the one-launch
-// form.  Per device, created on first use; if the runtime refuses a CU-masked stream the one-launch
-// form runs instead.
-struct PisSide {
-  bool ok = false;
-  hipStream_t roll = nullptr, base = nullptr;
-  hipEvent_t e0 = nullptr, eroll = nullptr, ebase = nullptr;
-};
-static bool pis_base_side_on() {
-  const char* e = std::getenv("DPI_PIS_BASE_SIDE");
-  return !e || std::atoi(e) != 0;
-}
-static PisSide* pis_side() {
-  static std::mutex mu;
-  static std::unordered_map<int, PisSide> per_dev;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = per_dev.find(dev);
-  if (it == per_dev.end()) {
-    PisSide s;
-    const int ncu = cu_count(), words = (ncu + 31) / 32;
-    constexpr int BASE_CUS = 1;
-    std::vector<uint32_t> mroll(words, 0u), mbase(words, 0u);
-    for (int c = 0; c < ncu; ++c) (c < BASE_CUS ? mbase : mroll)[c >> 5] |= 1u << (c & 31);
-    s.ok = ncu > 8 && hipExtStreamCreateWithCUMask(&s.roll, (uint32_t)words, mroll.data()) == hipSuccess &&
-           hipExtStreamCreateWithCUMask(&s.base, (uint32_t)words, mbase.data()) == hipSuccess &&
-           hipEventCreateWithFlags(&s.e0, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.eroll, hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&s.ebase, hipEventDisableTiming) == hipSuccess;
-    (void)hipGetLastError();  // a refused mask leaves s.ok false, not a sticky error
-    it = per_dev.emplace(dev, s).first;
-  }
-  return it->second.ok ? &it->second : nullptr;
-}
-
 // prepared: dpi_label_prepare already ran the first chunk's rollout and baseline rows (same
 // arguments, same workspace); prepare_only: run just those (dpi_label_prepare).
 static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
@@ -1254,7 +1211,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     auto chain = [&](bool vjp, int R) {
       return X3 ? pis_chain_x3(net->pis, rows, R, st, vjp) : pis_chain(net->pis, rows, R, st, vjp);
     };
-    auto rollout = [&](int stage, hipStream_t rs) {
+    auto rollout = [&](int stage) {
       // prepare stream: grids of pis_prep_per_cu() blocks per CU, so the rollout takes a bounded share
       // of each SIMD beside the previous batch's GEMM blocks instead of packing whole CUs (which
       // starves the GEMM)
@@ -1264,64 +1221,44 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       }
       for (int bx0 = 0; bx0 < g; bx0 += step) {
         if (pis_rollout_unroll() == 4)
-          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, rs, p->e,
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
                              net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
                              a.point_base, a.gx, rows, L, stage, dt, bx0);
         else
-          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, rs, p->e,
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
                              net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
                              a.point_base, a.gx, rows, L, stage, dt, bx0);
       }
     };
     const bool base = g0 == 0;
     float* brows = rows + (size_t)g * P * L.stride;
-    PisSide* side = nullptr;
-    if (X3 && base && !prepared && !prepare_only && dt == 0.f && pis_base_side_on() && pis_fused_on() &&
-        pis_fused_fits(net->pis, L))
-      side = pis_side();
-    if (side) {  // baseline chain on its CU beside the rollout (see PisSide)
-      HIPCHK(hipEventRecord(side->e0, st));
-      HIPCHK(hipStreamWaitEvent(side->base, side->e0, 0));
-      HIPCHK(hipStreamWaitEvent(side->roll, side->e0, 0));
-      hipLaunchKernelGGL(k_pis_points<X3>, dim3(n), dim3(64), 0, side->base, p->e.nx, net->pis, tx, n, brows, L);
-      const PisRows Lb = pis_chain_x3(net->pis, brows, n, side->base, true);
-      hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 63) / 64), dim3(256), 0, side->base, p->e,
-                         net->pis, brows, Lb, n, fb);
-      HIPCHK(hipEventRecord(side->ebase, side->base));
-      rollout(PIS_BOTH, side->roll);
-      HIPCHK(hipEventRecord(side->eroll, side->roll));
-      HIPCHK(hipStreamWaitEvent(st, side->eroll, 0));
-      const PisRows Lc = chain(true, g * P);
-      HIPCHK(hipStreamWaitEvent(st, side->ebase, 0));  // f_b
-      hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
-                         a.flags, fb, rows, Lc, a.partial, dt);
-      return 0;
-    }
     if (dt > 0.f) {
-      rollout(PIS_TD_TERM, st);
+      rollout(PIS_TD_TERM);
       if (a.flags & DPI_TERMINAL) {
         const PisRows Lt = chain(false, g * P);
         hipLaunchKernelGGL((k_pis_tvalue<DPI_EQ_OU, X3>), dim3(g), dim3(256), 0, st, p->e, net->pis, tx, g0, a.nbp,
                            a.gx, rows, Lt, g * P, dt);
       }
-      rollout(PIS_TD_INT, st);
+      rollout(PIS_TD_INT);
     } else if (!(prepared && base)) {
-      rollout(PIS_BOTH, st);
+      rollout(PIS_BOTH);
     }
     if (base && !(prepared && dt == 0.f))
       hipLaunchKernelGGL(k_pis_points<X3>, dim3(n), dim3(64), 0, st, p->e.nx, net->pis, tx, n, brows, L);
-    if (prepare_only) return 0;
+    if (prepare_only) return;
     const PisRows Lc = chain(true, g * P + (base ? n : 0));
     if (base)
       hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 63) / 64), dim3(256), 0, st, p->e, net->pis,
                          brows, Lc, n, fb);
     hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
                        a.flags, fb, rows, Lc, a.partial, dt);
-    return 0;
   };
   for (int g0 = 0; g0 < G; g0 += GC) {
     const int g = std::min(GC, G - g0);
-    if ((rc = x3 ? chunk(std::true_type{}, g0, g) : chunk(std::false_type{}, g0, g))) return rc;
+    if (x3)
+      chunk(std::true_type{}, g0, g);
+    else
+      chunk(std::false_type{}, g0, g);
     if (prepare_only) break;  // the first chunk only
   }
   HIPCHK(hipGetLastError());

@@ -179,33 +179,3 @@ def test_hjb_fused_chain_equals_layer_wise_chain(n, M, monkeypatch):
     assert torch.isfinite(out["1"][1]).all()
     assert torch.equal(out["0"][0], out["1"][0])
     assert torch.equal(out["0"][1], out["1"][1])
-
-
-@pytest.mark.parametrize("n,M", [(64, 4096), (3, 128)])
-def test_hjb_baseline_chain_beside_rollout_equals_one_launch(n, M, monkeypatch):
-    """The per-point baseline rows' chain on its own CU-masked stream beside the rollout
-    (DPI_PIS_BASE_SIDE, the default) against the baseline rows riding in the path chunk's
-    k_pis_net launch as its last tile (DPI_PIS_BASE_SIDE=0): row results do not depend on the
-    launch that carries the row, so the moments and labels are bitwise equal."""
-    import deeppicarditeration_amd as dpi
-    from deeppicarditeration_amd import _lib as L
-    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
-                               alpha_scale=4.0)
-    torch.manual_seed(0)
-    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
-    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
-                                  n_estimate_integral=M, n_euler_steps=8, seed=7)
-    tx, _ = gen.sample_t_and_x(n, point_base=0)
-    out = {}
-    for side in ("0", "1", "1"):  # twice beside: the reused streams and events
-        monkeypatch.setenv("DPI_PIS_BASE_SIDE", side)
-        ws = gen.point_baseline(tx)
-        mom = gen.label_moments(tx, 0, M, 0, M, L.DPI_BOTH, ws)
-        y = gen.finalize(mom, M, L.DPI_BOTH, ws)
-        torch.cuda.synchronize()
-        if side in out:
-            assert torch.equal(out[side][1], y)
-        out[side] = (mom, y)
-    assert torch.isfinite(out["1"][1]).all()
-    assert torch.equal(out["0"][0], out["1"][0])
-    assert torch.equal(out["0"][1], out["1"][1])
