@@ -55,7 +55,7 @@ WORKLOADS = {
                                                            "nn_module VJP chain in one launch) + k_pis_final + "
                                                            "k_reduce per dpi_label_moments call",
                 desc="HJB 100d T=1 (OUProcessEquation + 5-component GMM), 64 points x 4096 MC paths per GPU, K=50, "
-                     "PISGradNet 4x512 (layer-wise MFMA GEMM pipeline) (BASELINE configs[2])"),
+                     "PISGradNet 4x512 (fp16-split MFMA pipeline: forward + VJP chain in one k_pis_net launch) (BASELINE configs[2])"),
     "gbm_hess": dict(cfg="configs[4] stretch (Malliavin Hessian labels)", eq="GBMEquationComplexExact", widths=[64] * 3,
                      points=64, m_per_gpu=1024, K=50, sdgd=0, hess=True, flop=5.14e6, peak="split",
                      kernel="k_paths<GBM,64,3,hessians> + k_reduce + k_reduce_hess per dpi_label_moments_hessians call",

@@ -120,7 +120,9 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
                        size_t n_params, dpi_net* out);
 /* PISGradNet(hidden_shapes, dim = nx, g0 = equation.g, T) for OUProcessEquation; params: host fp32 in
  * torch state-dict order (timestep_phase, timestep_coeff, t_encoder.{0,2}, smooth_net.{0,2,..,2(L+1)},
- * nn_module.{0,2,..,2L} weights and biases).  Runs as a layer-wise MFMA GEMM pipeline. */
+ * nn_module.{0,2,..,2L} weights and biases).  Runs as an MFMA pipeline: rollout, time networks, the
+ * nn_module forward + VJP chain (one k_pis_net launch with the activations in LDS for 1-4 hidden
+ * layers of 512 in the fp16-split mode, else layer-wise GEMMs), final contributions. */
 int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, const float* params,
                            size_t n_params, dpi_net* out);
 int dpi_net_destroy(dpi_net net);

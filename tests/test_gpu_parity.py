@@ -288,7 +288,7 @@ def test_gbm_config5_network_sdgd_vs_oracle(mlp_precision):
 
 @pytest.mark.parametrize("gemm_mode", [0, 1])
 def test_hjb_pisgradnet_config3_network_vs_oracle(gemm_mode):
-    """Config-3 network: PISGradNet 4 x 512 (layer-wise MFMA GEMM pipeline, fp32 and fp16-split),
+    """Config-3 network: PISGradNet 4 x 512 (MFMA pipeline, fp32 layer-wise GEMMs and the fp16-split k_pis_net chain),
     OU + GMM, K = 20."""
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd import _lib as L
