@@ -45,6 +45,9 @@ constexpr int P = DPI_PATH_BLOCK;  // 64 paths per workgroup
 constexpr int NTH = 256;           // threads per workgroup
 constexpr int SS = P + 4;          // LDS row stride of the [dim][path] noise tile (bank-conflict free)
 constexpr int WST = 136;           // LDS row stride of a staged weight chunk (WST/4 = 2 mod 4)
+#ifndef DPI_NOISE_UNROLL_FO
+#define DPI_NOISE_UNROLL_FO 2  // independent Philox chains per wave in the first-order k_paths noise loops
+#endif
 constexpr int NXP_MAX = 128;       // max padded state dimension
 constexpr int HMAX = 128;
 
@@ -1512,7 +1515,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   // two independent Philox chains per wave in the noise loops (2 % on the one- and two-wave-per-SIMD
   // kernels); the Hessian-label kernel's register allocation measured 4 % slower with it
-  constexpr int NOISE_UNROLL = HESS ? 1 : 2;  // (4 measured no faster for GBM)
+  constexpr int NOISE_UNROLL = HESS ? 1 : GBM ? 2 : DPI_NOISE_UNROLL_FO;  // (4 measured no faster for GBM)
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;

@@ -7,7 +7,7 @@ import tempfile
 from pathlib import Path
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-lib = Path(__file__).resolve().parents[1] / "deeppicarditeration_amd" / "libdpi_hip.so"
+lib = Path(sys.argv.pop(1)) if len(sys.argv) > 2 and sys.argv[1].endswith(".so") else Path(__file__).resolve().parents[1] / "deeppicarditeration_amd" / "libdpi_hip.so"
 with tempfile.TemporaryDirectory() as d:
     fb, co = f"{d}/fb.bin", f"{d}/gfx950.co"
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", str(lib), fb], check=True)
