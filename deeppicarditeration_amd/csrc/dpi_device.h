@@ -46,7 +46,9 @@ constexpr int NTH = 256;           // threads per workgroup
 constexpr int SS = P + 4;          // LDS row stride of the [dim][path] noise tile (bank-conflict free)
 constexpr int WST = 136;           // LDS row stride of a staged weight chunk (WST/4 = 2 mod 4)
 #ifndef DPI_NOISE_UNROLL_FO
-#define DPI_NOISE_UNROLL_FO 2  // independent Philox chains per wave in the first-order k_paths noise loops
+// independent Philox chains per wave in the first-order k_paths noise loops: 4 (r03ag same-box A/B,
+// 3 pairs: Burgers 0.3763-0.3777 -> 0.3740-0.3760 ms/step, configs[3] 10.354 -> 10.303; still 252 VGPRs)
+#define DPI_NOISE_UNROLL_FO 4
 #endif
 constexpr int NXP_MAX = 128;       // max padded state dimension
 constexpr int HMAX = 128;
@@ -1513,8 +1515,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   constexpr bool GBM = KIND == DPI_EQ_GBM;
-  // two independent Philox chains per wave in the noise loops (2 % on the one- and two-wave-per-SIMD
-  // kernels); the Hessian-label kernel's register allocation measured 4 % slower with it
+  // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
+  // kernels; 4 vs 2 for first-order problems: 0.5 %); the Hessian-label kernel's register allocation
+  // measured 4 % slower with 2
   constexpr int NOISE_UNROLL = HESS ? 1 : GBM ? 2 : DPI_NOISE_UNROLL_FO;  // (4 measured no faster for GBM)
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
