@@ -50,6 +50,9 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 // 3 pairs: Burgers 0.3763-0.3777 -> 0.3740-0.3760 ms/step, configs[3] 10.354 -> 10.303; still 252 VGPRs)
 #define DPI_NOISE_UNROLL_FO 4
 #endif
+#ifndef DPI_NOISE_UNROLL_GBM
+#define DPI_NOISE_UNROLL_GBM 2  // the same for GBM's one-wave-per-SIMD k_paths
+#endif
 constexpr int NXP_MAX = 128;       // max padded state dimension
 constexpr int HMAX = 128;
 
@@ -1518,7 +1521,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
   // kernels; 4 vs 2 for first-order problems: 0.5 %); the Hessian-label kernel's register allocation
   // measured 4 % slower with 2
-  constexpr int NOISE_UNROLL = HESS ? 1 : GBM ? 2 : DPI_NOISE_UNROLL_FO;  // (4 measured no faster for GBM)
+  constexpr int NOISE_UNROLL = HESS ? 1 : GBM ? DPI_NOISE_UNROLL_GBM : DPI_NOISE_UNROLL_FO;  // (4 measured no faster for GBM)
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
