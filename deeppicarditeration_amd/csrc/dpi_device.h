@@ -55,6 +55,9 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 // 0.811-0.814 ms/step, k_paths 783 -> 773 us; 376 VGPRs either way)
 #define DPI_NOISE_UNROLL_GBM 4
 #endif
+#ifndef DPI_NOISE_UNROLL_HESS
+#define DPI_NOISE_UNROLL_HESS 1  // the Hessian-label k_paths
+#endif
 constexpr int NXP_MAX = 128;       // max padded state dimension
 constexpr int HMAX = 128;
 
@@ -1523,7 +1526,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
   // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM); the Hessian-label kernel's register
   // allocation measured 4 % slower with 2
-  constexpr int NOISE_UNROLL = HESS ? 1 : GBM ? DPI_NOISE_UNROLL_GBM : DPI_NOISE_UNROLL_FO;
+  constexpr int NOISE_UNROLL = HESS ? DPI_NOISE_UNROLL_HESS : GBM ? DPI_NOISE_UNROLL_GBM : DPI_NOISE_UNROLL_FO;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
