@@ -15,6 +15,12 @@ at N > 1 is the weak-scaling variant, 4096 paths per GPU).
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Rehearsal of the N > 1 path on ONE GPU (RCCL refuses two ranks on one device):
+DPI_BENCH_BACKEND=gloo DPI_BENCH_SHARE_GPU=1 with torch.distributed.run --nproc-per-node 2 runs both
+ranks on cuda:0 with the gloo process group; everything above init_process_group — the sharding,
+ShardedLabeler's two-phase begin/end with its asynchronous all_gather_into_tensor, the timing
+all-reduce — is the code the RCCL run executes.
 """
 import argparse
 import json
@@ -214,7 +220,9 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
-    dev = torch.device(f"cuda:{local}")
+    backend = os.environ.get("DPI_BENCH_BACKEND", "nccl")  # "gloo": the one-GPU rehearsal (module docstring)
+    share = os.environ.get("DPI_BENCH_SHARE_GPU", "0") == "1"
+    dev = torch.device(f"cuda:{0 if share else local}")
     torch.cuda.set_device(dev)
     # PISGradNet workloads: the next batch's sampling and baseline run on a low-priority side stream
     # while this batch's GEMM chain runs on a high-priority one (HJB 6.19 -> 5.92 ms/step).  Not for
@@ -230,7 +238,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd import _lib as L
@@ -445,10 +456,16 @@ def main():
             "scaling": wl.get("scaling", "weak"),
             "vs_baseline": None,
             "dtype": "f32",
+            "workload_key": args.workload,
             "data": "synthetic (Philox-sampled collocation points; random-init ELU MLP, torch.manual_seed(0))",
             "config": {"workload": wl["desc"], "baseline_config": wl["cfg"],
                        "points": N_POINTS, "mc_paths_per_gpu": M_PER_GPU, "euler_steps": K_STEPS, "nx": NX,
                        "parallelism": f"mc-shard{world}", "per_gpu_value": value / world,
+                       "arithmetic": ("fp32 noise / Euler-Maruyama / label moments; network "
+                                      + ("on exact-fp32 MFMA" if os.environ.get("DPI_GEMM", "") == "f32" else
+                                         "GEMMs on fp16x3-split MFMA (x = hi + lo, hi*hi + hi*lo + lo*hi into one "
+                                         "fp32 accumulator, DESIGN.md §2.2)")),
+                       "process_group": None if dist is None else backend + (" (ranks share cuda:0)" if share else ""),
                        "schedule": ("two-phase, next batch prepared on a side stream" if args.prepare and pipelined
                                     else "two-phase (all-gather overlapped)" if pipelined else "one labels() call"),
                        "prewarm_steps": prewarm,

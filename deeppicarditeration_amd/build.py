@@ -62,5 +62,42 @@ def build(force=False, verbose=True):
     return OUT
 
 
+def kernel_resources(lib=OUT):
+    """Per-kernel resources of the built library's gfx950 code objects (amdhsa.kernels metadata):
+    a list of dicts with the demangled `name` and vgpr_count (VGPR + AGPR), agpr_count,
+    vgpr_spill_count, sgpr_spill_count, private_segment_fixed_size (scratch bytes per lane),
+    group_segment_fixed_size (LDS bytes), uses_dynamic_stack.  Host tools only (objcopy, the ROCm
+    LLVM bundler and readelf, c++filt); no GPU."""
+    import re
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    notes = ""
+    with tempfile.TemporaryDirectory() as d:
+        fb = f"{d}/fb.bin"
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", str(lib), fb], check=True)
+        data = Path(fb).read_bytes()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"  # one offload bundle per translation unit
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        for k, st in enumerate(starts):
+            part, co = f"{d}/p{k}.bin", f"{d}/c{k}.co"
+            Path(part).write_bytes(data[st:starts[k + 1] if k + 1 < len(starts) else len(data)])
+            r = subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+            if r.returncode == 0:
+                notes += subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                                        text=True).stdout
+    out = []
+    ints = ("vgpr_count", "agpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size",
+            "group_segment_fixed_size")
+    for item in re.split(r"\n\s+- \.agpr_count:", notes)[1:]:
+        item = ".agpr_count:" + item
+        meta = {k: re.search(r"\." + k + r":\s+(\S+)", item) for k in ints + ("name", "uses_dynamic_stack")}
+        rec = {k: (int(m.group(1)) if k in ints else m.group(1)) for k, m in meta.items() if m}
+        rec["mangled"] = rec["name"]
+        rec["name"] = subprocess.run(["c++filt", rec["name"]], capture_output=True, text=True).stdout.strip()
+        out.append(rec)
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)

@@ -274,6 +274,9 @@ int dpi_last_error(char* buf, size_t len) {
 
 int dpi_problem_destroy(dpi_problem p);
 int dpi_net_destroy(dpi_net net);
+}
+static void prep_tags_drop(const void* owner);  // dpi_label_prepare's records naming a destroyed handle
+extern "C" {
 
 static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
   auto* p = new dpi_problem_s();
@@ -371,6 +374,7 @@ int dpi_problem_set_estimate_delta_t(dpi_problem p, double delta_t) {
 
 int dpi_problem_destroy(dpi_problem p) {
   if (!p) return 0;
+  prep_tags_drop(p);
   for (void* d : p->dev) (void)hipFree(d);
   delete p;
   return 0;
@@ -770,6 +774,7 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
 
 int dpi_net_destroy(dpi_net net) {
   if (!net) return 0;
+  prep_tags_drop(net);
   if (net->blob) (void)hipFree(net->blob);
   if (net->status) (void)hipFree(net->status);
   delete net;
@@ -1176,15 +1181,14 @@ static int pis_rollout_unroll() {
   return v;
 }
 
-// Rollout blocks per CU in each prepare-stream grid (DPI_PIS_PREP_PER_CU, default 3).  One block per
-// CU left the next batch's rollout (≈ 4.5 ms at one wave per SIMD) longer than the GEMM chain it hides
-// under, so every chain waited ≈ 0.5 ms for it; same-box A/B of the HJB step (r03p): 1 → 5.23,
-// 2 → 5.09, 3 → 5.00–5.05, 4 → 5.07–5.11, 6 → 5.04–5.09, 8 → 5.12–5.13 ms.
+// Prepare-stream rollout in grids of DPI_PIS_PREP_PER_CU path sets per CU (0 / unset: one grid).
+// Round 3's k_gemm_x3 chain needed bounded grids (3 per CU) so the rollout did not pack whole CUs;
+// the one-wave rollout beside k_pis_net runs as one grid by default.
 static int pis_prep_per_cu() {
   static int v = -1;
   if (v < 0) {
     const char* e = std::getenv("DPI_PIS_PREP_PER_CU");
-    v = e ? std::max(1, std::min(8, std::atoi(e))) : 3;
+    v = e ? std::max(0, std::min(64, std::atoi(e))) : 0;
   }
   return v;
 }
@@ -1216,18 +1220,17 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       // of each SIMD beside the previous batch's GEMM blocks instead of packing whole CUs (which
       // starves the GEMM)
       int step = g;
-      if (prepare_only) {
-        step = pis_prep_per_cu() * cu_count();
-      }
-      for (int bx0 = 0; bx0 < g; bx0 += step) {
+      if (prepare_only && pis_prep_per_cu() > 0) step = pis_prep_per_cu() * cu_count();
+      for (int bx0 = 0; bx0 < g; bx0 += step) {  // two one-wave blocks (terminal, integral) per path set
+        const dim3 grid(2 * std::min(step, g - bx0)), block(P);
         if (pis_rollout_unroll() == 4)
-          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
-                             net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
-                             a.point_base, a.gx, rows, L, stage, dt, bx0);
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
+                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L,
+                             stage, dt, bx0);
         else
-          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), dim3(std::min(step, g - bx0)), dim3(NTH), 0, st, p->e,
-                             net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i,
-                             a.point_base, a.gx, rows, L, stage, dt, bx0);
+          hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
+                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L,
+                             stage, dt, bx0);
       }
     };
     const bool base = g0 == 0;
@@ -1364,22 +1367,31 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
 // arguments per workspace (host side: no device read, no sync); the prepared call must match them
 // and consumes the record, so a mismatched or repeated call fails with DPI_ERR_ARG instead of
 // producing labels from another batch's rollout.
+// The tag also records the GEMM mode the rows were staged under (split and fp32 rows differ in
+// layout): a precision switch between prepare and the prepared call fails instead of reading rows
+// laid out the other way.
 struct PrepTag {
   const void *p, *net, *tx;
-  int n, M, K, m_begin, m_end, flags;
+  int n, M, K, m_begin, m_end, flags, mode;
   uint64_t seed;
   uint32_t epoch, point_base;
   size_t ws_bytes;
   bool operator==(const PrepTag& o) const {
     return p == o.p && net == o.net && tx == o.tx && n == o.n && M == o.M && K == o.K && m_begin == o.m_begin &&
-           m_end == o.m_end && flags == o.flags && seed == o.seed && epoch == o.epoch && point_base == o.point_base &&
-           ws_bytes == o.ws_bytes;
+           m_end == o.m_end && flags == o.flags && mode == o.mode && seed == o.seed && epoch == o.epoch &&
+           point_base == o.point_base && ws_bytes == o.ws_bytes;
   }
 };
 static std::mutex g_prep_mu;
 static std::unordered_map<const void*, PrepTag>& prep_tags() {
   static std::unordered_map<const void*, PrepTag> m;
   return m;
+}
+
+static void prep_tags_drop(const void* owner) {
+  std::lock_guard<std::mutex> g(g_prep_mu);
+  for (auto it = prep_tags().begin(); it != prep_tags().end();)
+    it = (it->second.p == owner || it->second.net == owner) ? prep_tags().erase(it) : std::next(it);
 }
 
 static bool stages_prepare(dpi_problem p, dpi_net net) { return net->d.kind == 2 && !(p->td_dt > 0.f); }
@@ -1394,7 +1406,8 @@ int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   if (!stages_prepare(p, net)) return 0;  // nothing to stage: the fused path kernels do it all
   {
     std::lock_guard<std::mutex> g(g_prep_mu);
-    prep_tags()[ws] = PrepTag{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, seed, epoch, point_base, ws_bytes};
+    prep_tags()[ws] =
+        PrepTag{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, pis_x3(net) ? 1 : 0, seed, epoch, point_base, ws_bytes};
   }
   return pis_paths(p, net, tx, n, K, a, w, (char*)ws, (hipStream_t)stream, false, true);
 }
@@ -1402,8 +1415,16 @@ int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M,
 static int check_prepared(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                           uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, void* ws,
                           size_t ws_bytes) {
-  if (!(flags & DPI_PREPARED) || n == 0 || !p || !net || !stages_prepare(p, net)) return 0;
-  const PrepTag want{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, seed, epoch, point_base, ws_bytes};
+  if (!(flags & DPI_PREPARED)) {
+    // an unprepared call restages this workspace: a tag left from an unconsumed prepare no longer
+    // describes its rows
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    prep_tags().erase(ws);
+    return 0;
+  }
+  if (n == 0 || !p || !net || !stages_prepare(p, net)) return 0;
+  const PrepTag want{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, pis_x3(net) ? 1 : 0, seed, epoch, point_base,
+                     ws_bytes};
   std::lock_guard<std::mutex> g(g_prep_mu);
   auto it = prep_tags().find(ws);
   if (it == prep_tags().end())
@@ -1412,7 +1433,7 @@ static int check_prepared(dpi_problem p, dpi_net net, const float* tx, int n, in
   prep_tags().erase(it);
   if (!same)
     return fail(DPI_ERR_ARG, "label_moments: DPI_PREPARED arguments differ from the dpi_label_prepare call on this "
-                             "workspace (points, counters, MC range, flags or workspace size)");
+                             "workspace (points, counters, MC range, flags, GEMM precision or workspace size)");
   return 0;
 }
 

@@ -98,64 +98,84 @@ __device__ __forceinline__ void x3_put4(float* row, int reg, int j, const float 
   *reinterpret_cast<uint2*>(g + 4) = make_uint2(lw[0], lw[1]);
 }
 
-// One (point, 64-path block) of the rollout: bx = the block's index within the chunk.
-template <int KIND, bool X3, int UNR = 2>
-__device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
-                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
-                                                  uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
-                                                  uint32_t point_base, const float* __restrict__ gx,
-                                                  float* __restrict__ rows, const PisRows& L, int stage, float td_dt,
-                                                  float* xsh, float* gsts, int bx) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// The rollout of one (point, 64-path block) path set and ONE of its two paths, by one wave (lane =
+// path, no LDS): wave 2 g' + 0 rolls out the terminal path t -> T (S_T, g(X_T) -> a_p), wave
+// 2 g' + 1 the integral path t -> s (S_s, X_s -> the network input rows, s and its scalars).  The
+// point's x and the GMM parameters are wave-uniform (scalar loads), each lane's noise sums run over
+// k in order (the sum of dimension d is the same sequence of adds whatever wave owns d), and no
+// wave waits for another.  Block = one wave, so a rollout wave fits on any SIMD with 64 free VGPRs —
+// beside the previous batch's k_pis_net block (2 x <= 224 VGPRs, the whole LDS) on the prepare
+// stream (dpi_label_prepare).
+template <int KIND, bool X3, int UNR>
+__device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
+                                                 int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
+                                                 uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
+                                                 uint32_t point_base, const float* __restrict__ gx,
+                                                 float* __restrict__ rows, const PisRows& L, int stage, float td_dt,
+                                                 int bx, bool integral) {
+  const int lane = threadIdx.x & 63;
   const int g = g0 + bx;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
   const uint32_t ig = point_base + (uint32_t)i;
   const uint32_t m = (uint32_t)(m_begin + P * blk + lane);
   const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2;
   const bool TERM = flags & DPI_TERMINAL, INTG = flags & DPI_INTEGRAL;
-  const bool do_term = stage != PIS_TD_INT, do_int = stage != PIS_TD_TERM;
+  if (integral ? stage == PIS_TD_TERM : stage == PIS_TD_INT) return;
   const float* txr = tx + (size_t)i * F;
   const float t = txr[0], Kf = (float)K;
   bool td_u;
   const float tmt = pis_horizon(e, t, td_dt, td_u);
-  for (int d = tid; d < NXP_MAX; d += NTH) xsh[d] = d < nx ? txr[1 + d] : 0.f;
-  const size_t r = (size_t)bx * P + lane;
-  float* row = rows + r * L.stride;
+  float* row = rows + ((size_t)bx * P + lane) * L.stride;
+  if (!integral) {  // terminal path
+    const float cT = e.asq * sqrtf(tmt / Kf);
+    float gst[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
+    for (int j = 0; j < nb; ++j) {
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      if (TERM)
+#pragma unroll UNR
+        for (int k = 0; k < K; ++k) {
+          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3t, k0, k1));
+          s0 += z.a;
+          s1 += z.b;
+          s2 += z.c;
+          s3 += z.d;
+        }
+      const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+      float xv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * j + q;
+        xv[q] = d < nx ? fmaf(cT, sv[q], txr[1 + d]) : 0.f;
+        if (d < nx) {
+          row[L.ST + d] = sv[q];
+          if (TERM) Eq<KIND>::gstat(e, d, xv[q], gst);
+          if (!X3 && stage == PIS_TD_TERM) row[L.IN + PIS_IN_OFF + d] = xv[q];  // network input X_{t_next}
+        }
+      }
+      if (X3 && stage == PIS_TD_TERM) x3_put4(row, L.IN + 64, j, xv);
+    }
+    if (stage == PIS_TD_TERM) {  // the network at (t_next, X_{t_next}): time input and zero padding
+      if (X3) {
+        for (int j = nb; j < (L.INP - 64) / 4; ++j) {
+          const float z[4] = {0.f, 0.f, 0.f, 0.f};
+          x3_put4(row, L.IN + 64, j, z);
+        }
+        row[L.SC + 4] = t + td_dt;  // k_pis_time evaluates the time networks at T - tin
+      } else {
+        for (int j = 0; j < PIS_CH; ++j) pis_embed(pn, pn.T - (t + td_dt), row + L.E, j);
+      }
+    }
+    row[L.SC + 2] = TERM ? Eq<KIND>::gfin(e, gst) - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
+    return;
+  }
+  // integral path
   const float U = u01_oc(philox4x32_10(0u, m, ig, c3s, k0, k1).x);
   const float s = fmaf(U, tmt, t);
   const float smt = U * tmt;  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
   const float cI = e.asq * sqrtf(smt / Kf);
-  const float cT = e.asq * sqrtf(tmt / Kf);
-  __syncthreads();
-  float gst[NSG];
-#pragma unroll
-  for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
-  for (int j = wv; do_term && j < nb; j += 4) {  // terminal path
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (TERM)
-#pragma unroll UNR
-      for (int k = 0; k < K; ++k) {
-        const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3t, k0, k1));
-        s0 += z.a;
-        s1 += z.b;
-        s2 += z.c;
-        s3 += z.d;
-      }
-    const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
-    float xv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = 4 * j + q;
-      xv[q] = d < nx ? fmaf(cT, sv[q], xsh[d]) : 0.f;
-      if (d < nx) {
-        row[L.ST + d] = sv[q];
-        if (TERM) Eq<KIND>::gstat(e, d, xv[q], gst);
-        if (!X3 && stage == PIS_TD_TERM) row[L.IN + PIS_IN_OFF + d] = xv[q];  // network input X_{t_next}
-      }
-    }
-    if (X3 && stage == PIS_TD_TERM) x3_put4(row, L.IN + 64, j, xv);
-  }
-  for (int j = 3 - wv; do_int && j < nb; j += 4) {  // integral path
+  for (int j = 0; j < nb; ++j) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (INTG)
 #pragma unroll UNR
@@ -171,7 +191,7 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int d = 4 * j + q;
-      xv[q] = d < nx ? fmaf(cI, sv[q], xsh[d]) : 0.f;  // X_s
+      xv[q] = d < nx ? fmaf(cI, sv[q], txr[1 + d]) : 0.f;  // X_s
       if (d < nx) {
         row[L.SS + d] = sv[q];
         if (!X3) row[L.IN + PIS_IN_OFF + d] = xv[q];
@@ -179,55 +199,30 @@ __device__ __forceinline__ void pis_rollout_block(const EqDev& e, const NetPisDe
     }
     if (X3) x3_put4(row, L.IN + 64, j, xv);
   }
-  // split rows: the zero padding of the x part (dims nx .. INP - 64) of IN
-  if (X3)
-    for (int j = nb + wv; j < (L.INP - 64) / 4; j += 4) {
+  if (X3) {  // the zero padding of the x part (dims nx .. INP - 64) of IN; the time input
+    for (int j = nb; j < (L.INP - 64) / 4; ++j) {
       const float z[4] = {0.f, 0.f, 0.f, 0.f};
       x3_put4(row, L.IN + 64, j, z);
     }
-  // time embedding of lambda = T - s (each wave writes 16 of the 64 channels); the TD terminal
-  // stage evaluates the network at t_next
-  const float tin = stage == PIS_TD_TERM ? t + td_dt : s;
-  if (!X3)
-    for (int j = wv; j < PIS_CH; j += 4) pis_embed(pn, pn.T - tin, row + L.E, j);
-  else if (wv == 0)
-    row[L.SC + 4] = tin;  // k_pis_time evaluates the time networks at T - tin
-#pragma unroll
-  for (int c = 0; c < NSG; ++c) gsts[(wv * P + lane) * NSG + c] = gst[c];
-  __syncthreads();
-  if (wv == 0) {
-    float gT = 0.f;
-    if (TERM && do_term) {
-#pragma unroll
-      for (int c = 0; c < NSG; ++c)
-        gst[c] = ((gsts[(0 * P + lane) * NSG + c] + gsts[(1 * P + lane) * NSG + c]) + gsts[(2 * P + lane) * NSG + c]) +
-                 gsts[(3 * P + lane) * NSG + c];
-      gT = Eq<KIND>::gfin(e, gst);
-    }
-    if (do_int) {
-      row[L.SC + 0] = s;
-      row[L.SC + 1] = cI;
-      row[L.SC + 3] = smt;
-    }
-    if (do_term) row[L.SC + 2] = TERM ? gT - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
+    row[L.SC + 4] = s;  // k_pis_time evaluates the time networks at T - s
+  } else {
+    for (int j = 0; j < PIS_CH; ++j) pis_embed(pn, pn.T - s, row + L.E, j);
   }
+  row[L.SC + 0] = s;
+  row[L.SC + 1] = cI;
+  row[L.SC + 3] = smt;
 }
 
-// Block bx0 + blockIdx.x of the chunk.  8.7 KB of LDS (no staging of X_s); UNR independent Philox
-// chains per wave in the noise loops, capped at 64 VGPRs, so a rollout block (one wave per SIMD)
-// fits on a CU beside two k_gemm_x3h blocks (2 x 66 KB, 2 x 208 VGPRs per SIMD): the prepare stream
-// launches the next batch's rollout in grids of DPI_PIS_PREP_PER_CU (3) blocks per CU.
-template <int KIND, bool X3, int UNR = 2>
-__global__ __launch_bounds__(256, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
-                                                     int nbp, int m_begin, int K, int flags, uint32_t k0,
-                                                     uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
-                                                     uint32_t point_base, const float* __restrict__ gx,
-                                                     float* __restrict__ rows, PisRows L, int stage, float td_dt,
-                                                     int bx0) {
-  __shared__ float xsh[NXP_MAX];
-  __shared__ float gsts[4 * P * NSG];
-  pis_rollout_block<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L,
-                              stage, td_dt, xsh, gsts, bx0 + blockIdx.x);
+// Waves 2 (bx0 + b) and 2 (bx0 + b) + 1 of the chunk: one 64-thread block per wave.  UNR
+// independent Philox chains per wave in the noise loops, <= 64 VGPRs.
+template <int KIND, bool X3, int UNR = 4>
+__global__ __launch_bounds__(64, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
+                                                    int nbp, int m_begin, int K, int flags, uint32_t k0, uint32_t k1,
+                                                    uint32_t c3t, uint32_t c3s, uint32_t c3i, uint32_t point_base,
+                                                    const float* __restrict__ gx, float* __restrict__ rows, PisRows L,
+                                                    int stage, float td_dt, int bx0) {
+  pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows,
+                                  L, stage, td_dt, bx0 + (int)(blockIdx.x >> 1), blockIdx.x & 1);
 }
 
 // Baseline rows: IN[i] = [.., x], E[i] = emb(T - t), SC = (t, 1, 0, 0).

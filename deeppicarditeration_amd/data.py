@@ -139,6 +139,12 @@ class OnlineDataGenerator:
             raise ValueError(f"label_dtype must be float32 or float64 (got {label_dtype})")
         self.label_dtype = label_dtype
 
+    def __getstate__(self):
+        # DataLoader worker processes (DATA.N_WORKERS > 0, picard/data.py:1768-1779) would pickle the
+        # generator: its problem / network handles are device state of this process
+        raise TypeError("the HIP OnlineDataGenerator holds device handles of this process and cannot move to "
+                        "DataLoader worker processes: set DATA.N_WORKERS 0")
+
     def _configure_problem(self):
         """The device problem handle belongs to the equation and may be shared by several
         generators: (re)apply this generator's estimator settings before each label call."""

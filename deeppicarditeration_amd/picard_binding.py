@@ -68,6 +68,14 @@ def hip_online_data_generator(kws, data_cfg=None, base=None, generator_cls=None)
     solution, N, i = kw.pop("solution"), kw.pop("N"), kw.pop("i")
     device = kw.pop("device", "cuda")
     cap = int(_cfg_get(data_cfg, "POINTS_PER_CALL", DEFAULT_POINTS_PER_CALL))
+    workers = [int(_cfg_get(data_cfg, k, 0) or 0) for k in ("N_WORKERS", "PRELOAD_N_WORKERS")]
+    if max(workers) > 0:
+        # the reference's default is DATA.N_WORKERS 1 (picard/config.py:75): its DataLoader would then
+        # pickle the dataset into spawned worker processes (data.py:1542-1549, 1768-1779), and the
+        # HIP generator's problem / network handles are device state of this process
+        raise ValueError(f"DATA.BACKEND hip labels in the training process itself (one fused kernel per call, "
+                         f"no DataLoader workers): set DATA.N_WORKERS 0 (got N_WORKERS {workers[0]}, "
+                         f"PRELOAD_N_WORKERS {workers[1]}); every shipped DPI YAML sets N_WORKERS: 0")
     data_size = _cfg_get(data_cfg, "DATA_SIZE", None)
     n_buffer = _cfg_get(data_cfg, "N_BUFFER", None)
     if data_cfg is not None and not _cfg_get(data_cfg, "NEW_SAMPLING", False) and n_buffer in (None, 0) \

@@ -157,6 +157,10 @@ class ShardedLabeler:
             raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
         slot = wslot = None
         kflags = None
+        if not self._pipeline_pending():
+            # a pipeline starts: the range-status word must describe only its own batches
+            # (pipeline_range_check reads it once the pipeline is drained)
+            self._clear_range_status()
         if prepared is not None:
             tx, point_base, ws, ready, slot, pflags = prepared
             if flags is not None and flags != pflags:
@@ -197,6 +201,38 @@ class ShardedLabeler:
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
         work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
         return (ws, flat, work, tuple(mom.shape), flags, M, slot, wslot)
+
+    def _pipeline_pending(self):
+        return any(getattr(self, "_ws_busy", ())) or any(getattr(self, "_prep_busy", ()))
+
+    def _clear_range_status(self):
+        gen = self.gen
+        if getattr(gen, "range_check", False) and hasattr(gen, "range_status") and \
+                not torch.cuda.is_current_stream_capturing():
+            gen.range_status(clear=True)
+
+    def pipeline_range_check(self):
+        """The range guard for the pipelined path (prepare/begin/end), which cannot recompute a
+        batch once later ones are in flight: after the last end(), read and clear the net's status
+        word (a MAX all-reduce across ranks, like labels()) and raise DPIError if any pipelined
+        batch gave non-finite sums — rerun those batches with labels(), which falls back to fp32."""
+        gen = self.gen
+        if not getattr(gen, "range_check", False) or not hasattr(gen, "range_status"):
+            return 0
+        if self._pipeline_pending():
+            raise RuntimeError("pipeline_range_check(): end() every pending batch first")
+        from . import _lib
+        flag = gen.range_status(clear=True)
+        if self.world > 1:
+            import torch.distributed as dist
+            dev = "cpu" if dist.get_backend(self.group) == "gloo" else gen.device
+            t = torch.tensor([float(flag)], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            flag = int(t.item())
+        if flag & _lib.DPI_STATUS_NONFINITE:
+            raise _lib.DPIError("pipelined labels (begin/end) gave non-finite sums: the fp16-split evaluation left "
+                                "fp16's range; recompute those batches with labels(), which falls back to exact fp32")
+        return flag
 
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""

@@ -107,6 +107,14 @@ def test_unbounded_buffer_estimate_is_refused_up_front(results):
     assert "POINTS_PER_CALL" in results["n_buffer_unset"]["error"]
 
 
+def test_reference_default_n_workers_is_refused_with_the_fix_named(results):
+    """DATA.N_WORKERS defaults to 1 in the reference (picard/config.py:75); the HIP generator holds
+    device handles of the training process, so the binding refuses worker processes up front
+    instead of failing later inside the DataLoader's pickling."""
+    err = results["n_workers_default"]["error"]
+    assert err is not None and "N_WORKERS 0" in err
+
+
 def test_gbm_hessian_supervision(results):
     r = results["gbm_hessians"]
     assert r["equation"] == "deeppicarditeration_amd.equations.GBMEquationComplexExact"
