@@ -91,7 +91,7 @@ def parse():
     ap.add_argument("--prepare", action="store_true", help="two-phase labels with the next batch's sampling and "
                                                            "baseline on a low-priority side stream, the path "
                                                            "kernels on a high-priority stream")
-    ap.add_argument("--no-prepare", action="store_true", help="one stream (the default; overrides --prepare)")
+    ap.add_argument("--no-prepare", action="store_true", help="one stream (overrides --prepare and the hjb default)")
     return ap.parse_args()
 
 
@@ -229,9 +229,9 @@ def main():
     # the fused-kernel workloads, whose one path launch the side work would slow.
     if args.workload is None:
         args.workload = "burgers" if world == 1 else "burgers_cfg3"
-    # (hjb ran prepared by default while its chain was nine GEMM launches whose blocks left room for the
-    # next batch's rollout; k_pis_net holds a CU's whole LDS, so one stream is now as fast: DESIGN §2.4)
-    args.prepare = args.prepare and not args.no_prepare
+    # PISGradNet (hjb): the next batch's rollout runs on the side stream beside this batch's k_pis_net,
+    # one wave per SIMD (k_pis_rollout_shared) — the default for that workload
+    args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis"))) and not args.no_prepare
     if args.prepare:
         lo, hi = torch.cuda.Stream.priority_range()
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=hi))
@@ -370,6 +370,12 @@ def main():
         dt, k_ms = float(t[0]), float(t[1])
     assert torch.isfinite(y).all()
     parity = live_parity(wl, eq, net, capture["tx"], capture["pb"], capture["y"], M) if rank == 0 else None
+    if rank == 0 and world > 1:
+        # the sharded labels against ONE call over all M paths of the same batch on this GPU (after
+        # the timed region): bit-identical when M / (64 N) is a power of two
+        y1 = ShardedLabeler(gen, rank=0, world=1).labels(capture["tx"], capture["pb"])
+        parity["bit_identical_to_single_call"] = bool(torch.equal(y1, capture["y"]))
+        parity["max_abs_diff_to_single_call"] = float((y1 - capture["y"]).abs().max())
     # Noise floor of the same launch (untimed, after the timed region): the identical rollout with
     # u = 0 (ZeroSolution: same Philox streams, same K-step EM, no network), i.e. the
     # Philox4x32-10 + Box-Muller VALU issue the noise contract fixes.

@@ -454,20 +454,23 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
     for (int c = 0; c < NT / 2; ++c) {
       const int U = (n0 >> 5) + wn * (NT / 2) + c;
       float v[8];
+      // scale and bias as explicit FMAs (no contraction left to the compiler), so k_pis_net's
+      // epilogue reproduces these outputs bit for bit
+      float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if ((EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && has_bias) {
+        const int o = 32 * (wn * (NT / 2) + c) + 4 * ql;  // = 32 U + 4 ql - n0
+        const float* bsrc = LDS_BIAS ? sbias + o : bias + 32 * U + 4 * ql;
+        const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+        const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
+        bb[0] = b0.x, bb[1] = b0.y, bb[2] = b0.z, bb[3] = b0.w;
+        bb[4] = b1.x, bb[5] = b1.y, bb[6] = b1.z, bb[7] = b1.w;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = acc[2 * c][b][r] * wscale;
-        v[4 + r] = acc[2 * c + 1][b][r] * wscale;
+        v[r] = __builtin_fmaf(acc[2 * c][b][r], wscale, bb[r]);
+        v[4 + r] = __builtin_fmaf(acc[2 * c + 1][b][r], wscale, bb[4 + r]);
       }
       if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
-        if (has_bias) {
-          const int o = 32 * (wn * (NT / 2) + c) + 4 * ql;  // = 32 U + 4 ql - n0
-          const float* bsrc = LDS_BIAS ? sbias + o : bias + 32 * U + 4 * ql;
-          const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
-          const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
-          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
-          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
-        }
         if (EPI == EPI_BIAS_ELU)
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
@@ -668,19 +671,21 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3h(int M, int Kp, int 
     for (int c = 0; c < NT / 2; ++c) {
       const int U = (n0 >> 5) + wn * (NT / 2) + c;
       float v[8];
+      // scale and bias as explicit FMAs (as x3_tile)
+      float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if ((EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) && has_bias) {
+        const float* bsrc = sbias + 32 * (wn * (NT / 2) + c) + 4 * ql;
+        const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
+        const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
+        bb[0] = b0.x, bb[1] = b0.y, bb[2] = b0.z, bb[3] = b0.w;
+        bb[4] = b1.x, bb[5] = b1.y, bb[6] = b1.z, bb[7] = b1.w;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = acc[2 * c][b][r] * wscale;
-        v[4 + r] = acc[2 * c + 1][b][r] * wscale;
+        v[r] = __builtin_fmaf(acc[2 * c][b][r], wscale, bb[r]);
+        v[4 + r] = __builtin_fmaf(acc[2 * c + 1][b][r], wscale, bb[4 + r]);
       }
       if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
-        if (has_bias) {
-          const float* bsrc = sbias + 32 * (wn * (NT / 2) + c) + 4 * ql;
-          const float4 b0 = *reinterpret_cast<const float4*>(bsrc);
-          const float4 b1 = *reinterpret_cast<const float4*>(bsrc + 16);
-          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
-          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
-        }
         if (EPI == EPI_BIAS_ELU)
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;

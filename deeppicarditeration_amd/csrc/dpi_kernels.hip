@@ -840,7 +840,7 @@ static int pis_chunk_wg() {
 
 // Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | [PIS rows] | partial[n][2F][nbp]  (256-B aligned)
 struct WsLayout {
-  size_t gx, fb, bx, hb, rows, partial, total;
+  size_t gx, fb, bx, hb, rows, partial, rq, total;
   int rows_cap;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -862,7 +862,9 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
     rows_bytes = al256((size_t)w.rows_cap * stride * 4);
   }
   w.partial = w.rows + rows_bytes;
-  w.total = w.partial + (size_t)n * nbp * slab_row(F) * 4;
+  w.rq = w.partial + al256((size_t)n * nbp * slab_row(F) * 4);
+  // PISGradNet: the shared rollout's queue counter (256 B) and per-SIMD claim words
+  w.total = w.rq + ((net && net->d.kind == 2) ? 256 + (size_t)PIS_CLAIM_SLOTS * 4 : 0);
   return w;
 }
 
@@ -1011,10 +1013,22 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   if (vjp && R > 0 && pis_fused_on() && pis_fused_fits(pd, L)) {
     const dim3 grid((R + PN_BM - 1) / PN_BM), block(PN_THREADS);
     const char* e = std::getenv("DPI_PIS_NT");
-    if (!e || std::atoi(e) != 0)
-      hipLaunchKernelGGL(k_pis_net<true>, grid, block, 0, st, pd, rows, L, R);
+    const bool nt = !e || std::atoi(e) != 0;
+    auto launch = [&](auto ntc, auto nlc) {
+      hipLaunchKernelGGL((k_pis_net<decltype(ntc)::value, decltype(nlc)::value>), grid, block, 0, st, pd, rows, L, R);
+    };
+    auto by_depth = [&](auto ntc) {
+      switch (pd.L) {
+        case 1: launch(ntc, std::integral_constant<int, 1>{}); break;
+        case 2: launch(ntc, std::integral_constant<int, 2>{}); break;
+        case 3: launch(ntc, std::integral_constant<int, 3>{}); break;
+        default: launch(ntc, std::integral_constant<int, 4>{}); break;
+      }
+    };
+    if (nt)
+      by_depth(std::true_type{});
     else
-      hipLaunchKernelGGL(k_pis_net<false>, grid, block, 0, st, pd, rows, L, R);
+      by_depth(std::false_type{});
     return L;
   }
   int Kp = L.INP;
@@ -1193,6 +1207,30 @@ static int pis_prep_per_cu() {
   return v;
 }
 
+// The prepare stream's rollout as the per-SIMD-capped work queue (k_pis_rollout_shared), launched
+// with DPI_PIS_PREP_SHARED (default 2) waves per SIMD more than it keeps; 0: the plain grid.
+static int pis_prep_shared() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_PIS_PREP_SHARED");
+    v = e ? std::max(0, std::min(8, std::atoi(e))) : 2;
+  }
+  return v;
+}
+
+// Path sets of a prepared chunk the prepare stream rolls out: DPI_PIS_PREP_FRAC (default 0.92) of
+// them; the shared rollout beside k_pis_net runs at about a third of its stand-alone rate, so the
+// rest goes to the prepared call's head at full occupancy (r04f trace: the prepare-stream rollout
+// of the whole chunk, 4.07 ms, outlasted the 3.75 ms chain it hid under).
+static int pis_prep_sets(int g) {
+  static double f = -1.0;
+  if (f < 0.0) {
+    const char* e = std::getenv("DPI_PIS_PREP_FRAC");
+    f = e ? std::max(0.0, std::min(1.0, std::atof(e))) : 0.92;
+  }
+  return std::max(0, std::min(g, (int)(f * g + 0.5)));
+}
+
 // prepared: dpi_label_prepare already ran the first chunk's rollout and baseline rows (same
 // arguments, same workspace); prepare_only: run just those (dpi_label_prepare).
 static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, const PathArgs& a, const WsLayout& w,
@@ -1215,14 +1253,27 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     auto chain = [&](bool vjp, int R) {
       return X3 ? pis_chain_x3(net->pis, rows, R, st, vjp) : pis_chain(net->pis, rows, R, st, vjp);
     };
-    auto rollout = [&](int stage) {
-      // prepare stream: grids of pis_prep_per_cu() blocks per CU, so the rollout takes a bounded share
-      // of each SIMD beside the previous batch's GEMM blocks instead of packing whole CUs (which
-      // starves the GEMM)
-      int step = g;
+    // path sets [0, gprep) of a prepared first chunk roll out on the prepare stream (beside the
+    // previous batch's chain), the rest [gprep, g) at full occupancy at the head of the prepared
+    // call, so the two streams' critical paths balance (DPI_PIS_PREP_FRAC)
+    const int gprep = (prepare_only || prepared) ? pis_prep_sets(g) : g;
+    auto rollout = [&](int stage, int gbeg = 0) {
+      if constexpr (X3) {  // (k_pis_net, which it hides under, exists for the split rows only)
+        if (prepare_only && pis_prep_shared()) {
+          // the prepare stream: at most one rollout wave per SIMD beside the previous batch's chain
+          int* rq = (int*)(b + w.rq);
+          (void)hipMemsetAsync(rq, 0, 256 + (size_t)PIS_CLAIM_SLOTS * 4, st);
+          hipLaunchKernelGGL((k_pis_rollout_shared<DPI_EQ_OU, true>), dim3(4 * cu_count() * (1 + pis_prep_shared())),
+                             dim3(P), 0, st, p->e, net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t,
+                             a.c3s, a.c3i, a.point_base, a.gx, rows, L, stage, dt, 0, 2 * gprep, rq, rq + 64, 1);
+          return;
+        }
+      }
+      const int gend = prepare_only ? gprep : g;
+      int step = gend - gbeg;
       if (prepare_only && pis_prep_per_cu() > 0) step = pis_prep_per_cu() * cu_count();
-      for (int bx0 = 0; bx0 < g; bx0 += step) {  // two one-wave blocks (terminal, integral) per path set
-        const dim3 grid(2 * std::min(step, g - bx0)), block(P);
+      for (int bx0 = gbeg; bx0 < gend; bx0 += step) {  // two one-wave blocks (terminal, integral) per path set
+        const dim3 grid(2 * std::min(step, gend - bx0)), block(P);
         if (pis_rollout_unroll() == 4)
           hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
                              a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L,
@@ -1245,6 +1296,8 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       rollout(PIS_TD_INT);
     } else if (!(prepared && base)) {
       rollout(PIS_BOTH);
+    } else if (gprep < g) {
+      rollout(PIS_BOTH, gprep);  // the prepared chunk's remaining path sets
     }
     if (base && !(prepared && dt == 0.f))
       hipLaunchKernelGGL(k_pis_points<X3>, dim3(n), dim3(64), 0, st, p->e.nx, net->pis, tx, n, brows, L);

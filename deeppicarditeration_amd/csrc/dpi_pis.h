@@ -225,6 +225,58 @@ __global__ __launch_bounds__(64, 8) void k_pis_rollout(EqDev e, NetPisDev pn, co
                                   L, stage, td_dt, bx0 + (int)(blockIdx.x >> 1), blockIdx.x & 1);
 }
 
+// The prepare stream's rollout (dpi_label_prepare), beside the previous batch's k_pis_net: a
+// work queue of the 2 g one-wave tasks served by at most one wave per SIMD.  Left to the dispatcher,
+// the next batch's rollout waves fill every register a finishing k_pis_net block frees (up to nine
+// 56-VGPR waves per SIMD) and the next k_pis_net block waits for them: the chain stretched from 2.9
+// to 4.0 ms while the rollout ran at nearly its stand-alone speed (r04a) — zero-sum.  Here the first
+// wave of the launch on a SIMD (claim word per SIMD, keyed by HW_ID's SE / SH / CU / SIMD fields and
+// the XCC id; zeroed with the queue counter before the launch) takes tasks until the queue is
+// empty; every other wave leaves at once.  A SIMD then holds two k_pis_net waves (<= 232 registers
+// each) and one rollout wave (<= 48): the chain keeps its CU, and the rollout fills the VALU issue
+// slots the feed-bound chain leaves idle.  Every wave reaches the exit: a claimed wave ends when the
+// queue counter passes ntask, an unclaimed one immediately.
+constexpr int PIS_CLAIM_SLOTS = 8 * 256 * 4;  // XCC x (SE, SH, CU) x SIMD
+template <int KIND, bool X3, int UNR>
+__device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0, int nbp,
+                                                            int m_begin, int K, int flags, uint32_t k0,
+                                                           uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
+                                                           uint32_t point_base, const float* __restrict__ gx,
+                                                           float* __restrict__ rows, PisRows L, int stage, float td_dt,
+                                                           int bx0, int ntask, int* __restrict__ queue,
+                                                           int* __restrict__ claim, int waves) {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);         // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+  const unsigned slot = (xcc << 10) | (((hw >> 8) & 0xffu) << 2) | ((hw >> 4) & 3u);
+  const int lane = threadIdx.x & 63;
+  int old = 0;
+  if (lane == 0) old = atomicAdd(claim + slot, 1);
+  if (__shfl(old, 0, 64) >= waves) return;  // this SIMD already runs `waves` rollout waves of this launch
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(queue, 1);
+    t = __shfl(t, 0, 64);
+    if (t >= ntask) break;
+    pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows,
+                                    L, stage, td_dt, bx0 + (t >> 1), t & 1);
+  }
+}
+
+#define DPI_PIS_SHARED_ARGS                                                                                         \
+  EqDev e, NetPisDev pn, const float *__restrict__ tx, int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,  \
+      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i, uint32_t point_base, const float *__restrict__ gx,      \
+      float *__restrict__ rows, PisRows L, int stage, float td_dt, int bx0, int ntask, int *__restrict__ queue,     \
+      int *__restrict__ claim, int waves
+#define DPI_PIS_SHARED_CALL \
+  e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L, stage, td_dt, bx0, ntask, queue, claim, waves
+// one wave per SIMD: 4 Philox chains per wave, <= 48 registers (beside two 232-register k_pis_net waves)
+template <int KIND, bool X3>
+__global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(24))) void k_pis_rollout_shared(DPI_PIS_SHARED_ARGS) {
+  pis_rollout_shared_body<KIND, X3, 4>(DPI_PIS_SHARED_CALL);
+}
+#undef DPI_PIS_SHARED_ARGS
+#undef DPI_PIS_SHARED_CALL
+
 // Baseline rows: IN[i] = [.., x], E[i] = emb(T - t), SC = (t, 1, 0, 0).
 template <bool X3>
 __global__ void k_pis_points(int nx, NetPisDev pn, const float* __restrict__ tx, int n, float* __restrict__ rows,

@@ -69,9 +69,15 @@ __device__ __forceinline__ void pn_split8(const float (&v)[8], u32x4_t& h, u32x4
   }
 }
 
-// Weight fragment register sets of pn_gemm (NT <= 4 unit tiles): three, rotating.
+// Weight fragment register sets of pn_gemm (NT <= 4 unit tiles), rotating: PN_WSETS = 3 keeps the
+// weights two chunks ahead, 2 one chunk ahead (32 registers fewer).
+#ifndef DPI_PN_WSETS
+#define DPI_PN_WSETS 3
+#endif
+constexpr int PN_WSETS = DPI_PN_WSETS;
+static_assert(PN_WSETS == 2 || PN_WSETS == 3, "weight register sets");
 struct PnW {
-  pn_h8 ah[3][4], al[3][4];
+  pn_h8 ah[PN_WSETS][4], al[PN_WSETS][4];
 };
 // set S <- chunk c of tiles T0 .. T0 + NT - 1 of a fragment-major matrix (pack_frag_major) with nkw
 // chunks per row behind rw: lane l's 16 B of each 1 KB block (one VGPR offset for every load; tile,
@@ -105,23 +111,27 @@ __device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], PnW& w, __amdgpu_b
   const int sw = x3_swz(il);  // = x3_swz(p0 + 16 b + il): p0 % 16 == 0
   const int oh = (p0 + il) * 32 + 4 * ((2 * ql) ^ sw), ol = (p0 + il) * 32 + 4 * ((2 * ql + 1) ^ sw);
   auto ldw = [&](int c, auto Sc) { pn_ldw<NT, decltype(Sc)::value>(w, rw, vo, T0, nkw, c0 + min(c, nk - 1)); };
+  // B fragments two path tiles at a time: tile b + 2's pair is read while tile b's MFMAs run
   auto mm = [&](int c, auto Sc) {
     constexpr int S = decltype(Sc)::value;
     const uint32_t* s = slab(c);
-    pn_h8 bh[NB], bl[NB];
+    pn_h8 bh[2], bl[2];
+    auto ldb = [&](int b) {
+      bh[b & 1] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + oh + 512 * b));
+      bl[b & 1] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + ol + 512 * b));
+    };
+    ldb(0);
+    if (NB > 1) ldb(1);
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      bh[b] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + oh + 512 * b));
-      bl[b] = __builtin_bit_cast(pn_h8, *reinterpret_cast<const u32x4_t*>(s + ol + 512 * b));
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bh[b], acc[t][b], 0, 0, 0);
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bl[b], acc[t][b], 0, 0, 0);
-        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.al[S][t], bh[b], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bh[b & 1], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.ah[S][t], bl[b & 1], acc[t][b], 0, 0, 0);
+        acc[t][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.al[S][t], bh[b & 1], acc[t][b], 0, 0, 0);
       }
+      if (b + 2 < NB) ldb(b + 2);
+    }
   };
   constexpr std::integral_constant<int, 0> I0{};
   constexpr std::integral_constant<int, 1> I1{};
@@ -129,23 +139,38 @@ __device__ __forceinline__ void pn_gemm(pn_f4 (&acc)[NT][NB], PnW& w, __amdgpu_b
   // sched_barrier(0): the scheduler keeps each load group where it is written (left alone it sinks
   // every load next to its first use to shorten live ranges)
   int c = 0;
+  if constexpr (PN_WSETS == 3) {
 #pragma unroll 1
-  for (; c + 3 <= nk; c += 3) {
-    ldw(c + 2, I2);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(c, I0);
-    __builtin_amdgcn_sched_barrier(0);
-    ldw(c + 3, I0);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(c + 1, I1);
-    __builtin_amdgcn_sched_barrier(0);
-    ldw(c + 4, I1);
-    __builtin_amdgcn_sched_barrier(0);
-    mm(c + 2, I2);
-    __builtin_amdgcn_sched_barrier(0);
+    for (; c + 3 <= nk; c += 3) {
+      ldw(c + 2, I2);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(c, I0);
+      __builtin_amdgcn_sched_barrier(0);
+      ldw(c + 3, I0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(c + 1, I1);
+      __builtin_amdgcn_sched_barrier(0);
+      ldw(c + 4, I1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(c + 2, I2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c < nk) mm(c, I0);
+    if (c + 1 < nk) mm(c + 1, I1);
+  } else {
+#pragma unroll 1
+    for (; c + 2 <= nk; c += 2) {
+      mm(c, I0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 2 < nk) ldw(c + 2, I0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(c + 1, I1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 3 < nk) ldw(c + 3, I1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (c < nk) mm(c, I0);
   }
-  if (c < nk) mm(c, I0);
-  if (c + 1 < nk) mm(c + 1, I1);
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -159,56 +184,55 @@ __device__ __forceinline__ void pn_zero(pn_f4 (&acc)[NT][NB]) {
 
 enum { PN_ELU = 0, PN_DELU_LDS = 1, PN_DELU_HBM = 2 };
 
-// row traffic (IN, the saved activations, GX) with the non-temporal hint when NTS, so the streams
-// through L2 do not evict the chain's weights (7 MB, shared by every block of the XCD)
+// Row traffic (IN, the saved activations, GX) goes through a buffer resource based at the block's
+// first row and sized to its valid rows: rows past R read as zeros and their stores are dropped, so
+// the partial last tile needs no clamped addresses, and every access is one 32-bit lane offset plus
+// a wave-uniform scalar offset (no 64-bit per-lane pointers held across the layers).  NTS: the
+// non-temporal hint (cache policy nt), so the row streams through L2 do not evict the chain's
+// weights (7 MB, shared by every block of the XCD).
 template <bool NTS>
-__device__ __forceinline__ u32x4_t pn_ld(const u32x4_t* p) {
-  if constexpr (NTS) return __builtin_nontemporal_load(p);
-  return *p;
+__device__ __forceinline__ u32x4_t pn_ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, NTS ? 2 : 0));
 }
 template <bool NTS>
-__device__ __forceinline__ void pn_st(u32x4_t* p, u32x4_t v) {
-  if constexpr (NTS)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
+__device__ __forceinline__ void pn_st(__amdgpu_buffer_rsrc_t r, int vo, int so, u32x4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, vo,
+                                         so, NTS ? 2 : 0);
 }
 
 // R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.  NTS: the non-temporal hint on
-// the row traffic (DPI_PIS_NT, default on).
-template <bool NTS>
-__global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* __restrict__ rows, PisRows L, int R) {
+// the row traffic (DPI_PIS_NT, default on).  At most 232 registers per wave (VGPRs + AGPRs; the
+// 160 KB of LDS leave none for another block): a one-wave k_pis_rollout_shared block of the next
+// batch (<= 48 VGPRs, no LDS) fits on every SIMD beside the two k_pis_net waves (2 x 232 + 48 =
+// 512).  (On gfx950 amdgpu_num_vgpr(N) caps the unified VGPR + AGPR file at 2 N: 116 -> 232; at 224
+// the allocator spilled one to five values whatever the code shape.)
+#ifndef DPI_PN_VGPR_HALF
+#define DPI_PN_VGPR_HALF 116  // 232 registers
+#endif
+template <bool NTS, int NL>
+__global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_PN_VGPR_HALF))) void k_pis_net(NetPisDev pd,
+                                                                                                 float* __restrict__ rows,
+                                                                                                 PisRows L, int R) {
+  // NL = pd.L hidden layers (host-dispatched): a template parameter, so the layer loops unroll
   __shared__ PnLds lds;
   const int tid = threadIdx.x, lane = tid & 63, il = lane & 15, ql = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = blockIdx.x * PN_BM, mrows = min(PN_BM, R - m0);
-  const size_t ld = (size_t)L.stride;
+  const int ldb = L.stride * 4;  // row stride in bytes
   const int nxk = L.INP / 32 - 2;  // chunks of X (1 .. PN_XC; host-checked)
-  float* const rbase = rows + (size_t)m0 * ld;
+  float* const rbase = rows + (size_t)m0 * L.stride;
+  const __amdgpu_buffer_rsrc_t rr = pn_rsrc(rbase, (size_t)mrows * ldb);
   // above any co-resident wave of another kernel, as the layer-wise GEMMs
   __builtin_amdgcn_s_setprio(2);
   auto act = [&](int c) -> uint32_t* { return lds.act + c * PN_SLAB; };
   auto xsl = [&](int c) -> uint32_t* { return lds.xs + c * PN_SLAB; };
-  // thread tid moves granule tid & 7 of tile row tid >> 3 in each chunk of a row region
+  // whole row regions: thread tid moves granule tid & 7 of tile row tid >> 3 in each chunk
   const int gr = tid >> 3, gg = tid & 7;
-  const int grc = min(gr, mrows - 1);  // rows past R load the last row (results discarded)
-  auto gsrc = [&](int reg, int c) {
-    return reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint32_t*>(rbase + (size_t)grc * ld + reg) + 32 * c +
-                                            4 * gg);
-  };
+  const int vrow = gr * ldb + 16 * gg;                        // + scalar 4 (reg + 32 c)
   auto gdst = [&](uint32_t* slab) { return reinterpret_cast<u32x4_t*>(slab + gr * 32 + 4 * (gg ^ x3_swz(gr))); };
-
-  // IN: the time embedding (chunks 0, 1) -> act, X (chunks 2 ..) -> xs
-  {
-    u32x4_t v[2 + PN_XC];
-#pragma unroll
-    for (int c = 0; c < 2 + PN_XC; ++c)
-      if (c < 2 + nxk) v[c] = pn_ld<NTS>(gsrc(L.IN, c));
-#pragma unroll
-    for (int c = 0; c < 2 + PN_XC; ++c)
-      if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
-  }
-  pn_barrier();
+  // a lane's own granule pairs of the 512-wide regions: row 16 b + il, chunk 2 wv + c, pair ql
+  const int vown = il * ldb + 32 * ql;                        // + scalar 16 b ldb + 4 reg + 128 (2 wv + c)
+  auto sown = [&](int reg, int b, int c) { return 16 * b * ldb + 4 * reg + 128 * (2 * wv + c); };
 
   // the 512-wide products: wave wv owns units 64 wv .. 64 wv + 63 (4 unit tiles) of all 64 rows
   pn_f4 acc[4][4];
@@ -227,70 +251,74 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
       pn_pre<4>(w, wsrc(pd.nnF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC);
   };
   auto pre_vjp = [&](int l) {  // D_{l-1} = (nnT[l] D_l) * elu'(A_{l-1}); l == L: from X
-    if (l == pd.L)
+    if (l == NL)
       pn_pre<4>(w, wsrc(pd.nnTF[l], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk);
     else
       pn_pre<4>(w, wsrc(pd.nnTF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC);
   };
   auto pre_gx = [&](int c0) { pn_pre<1>(w, rg, vo, min(wv, nopt - 1), KG / 32, c0, PN_HC); };
 
-  // epilogue of a 512-wide product, in two halves: values -> split words in registers (and the HBM
-  // copy) before the barrier that releases the layer input, the LDS stores after it.  Lane (il, ql)
+  // epilogue of a 512-wide product, one (path tile b, chunk c) at a time after the barrier that
+  // releases the layer input: values -> split words -> the HBM copy and the LDS image.  Lane (il, ql)
   // of path tile b holds units 64 wv + 16 t + 4 ql + r of row 16 b + il; unit tiles (2 c, 2 c + 1)
-  // form granule pair ql of chunk U = 2 wv + c.
-  u32x4_t eh[4][2], el[4][2];
+  // form granule pair ql of chunk U = 2 wv + c.  xh / xl: elu'(A) operands from HBM (kind
+  // PN_DELU_HBM); PN_DELU_LDS reads them from the lane's own granules of the image it overwrites.
   auto lds_at = [&](int b, int c, int hl) {
     const int m = 16 * b + il;
     return reinterpret_cast<u32x4_t*>(act(2 * wv + c) + m * 32 + 4 * ((2 * ql + hl) ^ x3_swz(m)));
   };
-  auto epi_values = [&](int kind, float ws, const float* bias, int save_reg, const u32x4_t (&xh)[4][2],
-                        const u32x4_t (&xl)[4][2]) {
+  auto epilogue = [&](int kind, float ws, const float* bias, int save_reg, const u32x4_t (&xh)[4][2],
+                      const u32x4_t (&xl)[4][2]) {
+    const __amdgpu_buffer_rsrc_t rb = pn_rsrc(bias, 4 * PN_H);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      const int m = 16 * b + il;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int U = 2 * wv + c;
         float v[8];
+        if (kind == PN_ELU) {  // k_gemm_x3h's EPI_BIAS_ELU arithmetic: fma(acc, 2^-s, bias), then ELU
+          // (a float vector, indexed: clang's __builtin_bit_cast of a vector ELEMENT reads element 0)
+          const pn_f4 b0 = __builtin_bit_cast(pn_f4, __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * ql, 128 * U, 0));
+          const pn_f4 b1 = __builtin_bit_cast(pn_f4, __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * ql, 128 * U + 64, 0));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[2 * c][b][r] * ws;
-          v[4 + r] = acc[2 * c + 1][b][r] * ws;
-        }
-        if (kind == PN_ELU) {
-          const float4 b0 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql);
-          const float4 b1 = *reinterpret_cast<const float4*>(bias + 32 * U + 4 * ql + 16);
-          v[0] += b0.x, v[1] += b0.y, v[2] += b0.z, v[3] += b0.w;
-          v[4] += b1.x, v[5] += b1.y, v[6] += b1.z, v[7] += b1.w;
+          for (int r = 0; r < 4; ++r) {
+            v[r] = __builtin_fmaf(acc[2 * c][b][r], ws, b0[r]);
+            v[4 + r] = __builtin_fmaf(acc[2 * c + 1][b][r], ws, b1[r]);
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
-        } else {
+        } else {  // EPI_DELU: (acc 2^-s) elu'(A)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = __builtin_fmaf(acc[2 * c][b][r], ws, 0.f);
+            v[4 + r] = __builtin_fmaf(acc[2 * c + 1][b][r], ws, 0.f);
+          }
+          u32x4_t ah, al;
+          if (kind == PN_DELU_LDS) {
+            ah = *lds_at(b, c, 0);
+            al = *lds_at(b, c, 1);
+          } else {
+            ah = xh[b][c];
+            al = xl[b][c];
+          }
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float a = x3_join(xh[b][c][j >> 1], xl[b][c][j >> 1], j & 1);
+            const float a = x3_join(ah[j >> 1], al[j >> 1], j & 1);
             v[j] *= a > 0.f ? 1.0f : a + 1.0f;
           }
         }
-        pn_split8(v, eh[b][c], el[b][c]);
-        if (save_reg >= 0 && m < mrows) {
-          u32x4_t* g = reinterpret_cast<u32x4_t*>(reinterpret_cast<uint32_t*>(rbase + (size_t)m * ld + save_reg) + 32 * U +
-                                                  8 * ql);
-          pn_st<NTS>(g, eh[b][c]);
-          pn_st<NTS>(g + 1, el[b][c]);
+        u32x4_t eh, el;
+        pn_split8(v, eh, el);
+        if (save_reg >= 0) {  // rows past R: dropped by the buffer's range check
+          pn_st<NTS>(rr, vown, sown(save_reg, b, c), eh);
+          pn_st<NTS>(rr, vown, sown(save_reg, b, c) + 16, el);
         }
+        *lds_at(b, c, 0) = eh;
+        *lds_at(b, c, 1) = el;
       }
     }
   };
-  auto epi_store = [&]() {
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        *lds_at(b, c, 0) = eh[b][c];
-        *lds_at(b, c, 1) = el[b][c];
-      }
-  };
-  u32x4_t xh[4][2], xl[4][2];  // elu' operands of the VJP epilogues
+  u32x4_t xh[4][2], xl[4][2];  // elu' operands of the PN_DELU_HBM epilogues
 
   pre_fwd(0);
   // IN: the time embedding (chunks 0, 1) -> act, X (chunks 2 ..) -> xs
@@ -298,7 +326,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     u32x4_t v[2 + PN_XC];
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
-      if (c < 2 + nxk) v[c] = pn_ld<NTS>(gsrc(L.IN, c));
+      if (c < 2 + nxk) v[c] = pn_ld<NTS>(rr, vrow, 4 * (L.IN + 32 * c));
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
       if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
@@ -306,73 +334,66 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
   pn_barrier();
 
   // forward
-  for (int l = 0; l < pd.L; ++l) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     pn_zero(acc);
     if (l == 0)
       pn_gemm<4, 4>(acc, w, wsrc(pd.nnF[0], PN_H, L.INP), vo, 4 * wv, L.INP / 32, 0, 2 + nxk, 0, il, ql,
                     [&](int c) { return c < 2 ? act(c) : xsl(c - 2); });
     else
       pn_gemm<4, 4>(acc, w, wsrc(pd.nnF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC, 0, il, ql, act);
-    if (l + 1 < pd.L)
+    if (l + 1 < NL)
       pre_fwd(l + 1);
     else
-      pre_vjp(pd.L);
-    epi_values(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], xh, xl);
+      pre_vjp(NL);
     pn_barrier();  // every wave's reads of the layer input are done
-    epi_store();
+    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], xh, xl);
     pn_barrier();
   }
   // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
   // granules, so no barrier before the stores)
   {
     pn_zero(acc);
-    pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[pd.L], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk, 0, il, ql, xsl);
+    pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[NL], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk, 0, il, ql, xsl);
     // the forward's HBM stores of A_0 .. A_{L-1} complete (read back below: A_{l-1} by the lane that
     // stored it, A_{L-1} by other waves for GX)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        xh[b][c] = *lds_at(b, c, 0);
-        xl[b][c] = *lds_at(b, c, 1);
-      }
-    if (pd.L > 1)
-      pre_vjp(pd.L - 1);
+    if (NL > 1)
+      pre_vjp(NL - 1);
     else
       pre_gx(0);
-    epi_values(PN_DELU_LDS, pd.nnTW[pd.L], nullptr, -1, xh, xl);
-    epi_store();
+    epilogue(PN_DELU_LDS, pd.nnTW[NL], nullptr, -1, xh, xl);
     pn_barrier();
   }
-  for (int l = pd.L - 1; l >= 1; --l) {
+#pragma unroll
+  for (int l = NL - 1; l >= 1; --l) {
     pn_zero(acc);
     pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[l], PN_H, PN_H), vo, 4 * wv, PN_HC, 0, PN_HC, 0, il, ql, act);
-    // elu'(A_{l-1}): this lane's own HBM copy, issued before the next weights so the counted wait
-    // for it leaves those in flight
+    // elu'(A_{l-1}): this lane's own HBM copy, issued before the next weights
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const u32x4_t* g = reinterpret_cast<const u32x4_t*>(
-            reinterpret_cast<const uint32_t*>(rbase + (size_t)min(16 * b + il, mrows - 1) * ld + L.A[l - 1]) +
-            32 * (2 * wv + c) + 8 * ql);
-        xh[b][c] = pn_ld<NTS>(g);
-        xl[b][c] = pn_ld<NTS>(g + 1);
+        xh[b][c] = pn_ld<NTS>(rr, vown, sown(L.A[l - 1], b, c));
+        xl[b][c] = pn_ld<NTS>(rr, vown, sown(L.A[l - 1], b, c) + 16);
       }
     if (l > 1)
       pre_vjp(l - 1);
     else
       pre_gx(0);
-    epi_values(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, xh, xl);
     pn_barrier();
-    epi_store();
+    epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, xh, xl);
     pn_barrier();
   }
   // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act).
   // Wave wv < nopt takes unit tile wv for all 64 rows, so each weight fragment is read once per
   // block; the two tiles of a granule pair then meet in the X image (free since D_{L-1}) as fp32.
   {
+    // the lane's (il, ql) again from the hardware lane count: keeping them live across the whole
+    // chain cost the register allocator a spill at the 224-register cap
+    int lid;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+    const int il = lid & 15, ql = lid >> 4;
     pn_f4 ag[1][4];
     pn_zero(ag);
     const bool live = wv < nopt;
@@ -381,7 +402,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     {
       u32x4_t v[PN_HC];
 #pragma unroll
-      for (int c = 0; c < PN_HC; ++c) v[c] = pn_ld<NTS>(gsrc(L.A[pd.L - 1], c));
+      for (int c = 0; c < PN_HC; ++c) v[c] = pn_ld<NTS>(rr, vrow, 4 * (L.A[NL - 1] + 32 * c));
       pn_barrier();
 #pragma unroll
       for (int c = 0; c < PN_HC; ++c) *gdst(act(c)) = v[c];
@@ -390,13 +411,12 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
     float* gx = reinterpret_cast<float*>(lds.xs);  // row m: 128 fp32
     if (live) {
       pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, PN_HC, PN_HC, 0, il, ql, act);
-      const float* bias = pd.nnbP[pd.L] + 16 * wv + 4 * ql;
+      const float* bias = pd.nnbP[NL] + 16 * wv + 4 * ql;
 #pragma unroll
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = ag[0][b][r] * pd.gxnoW;  // k_gemm_x3h's EPI_BIAS arithmetic
-          v += bias[r];
+          const float v = __builtin_fmaf(ag[0][b][r], pd.gxnoW, bias[r]);  // k_gemm_x3h's EPI_BIAS arithmetic
           gx[(16 * b + il) * 128 + 16 * wv + 4 * ql + r] = v;
         }
     }
@@ -409,7 +429,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) void k_pis_net(NetPisDev pd, float* 
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = gx[m * 128 + 32 * U + 4 * q + (j & 3) + 16 * (j >> 2)];
-      x3_put8(rbase + (size_t)m * ld, L.GX, U, q, v);
+      x3_put8(rbase + (size_t)m * L.stride, L.GX, U, q, v);
     }
   }
 }

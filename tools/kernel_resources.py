@@ -6,7 +6,7 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from deeppicarditeration_amd.build import OUT, kernel_resources  # noqa: E402
 
-lib = Path(sys.argv.pop(1)) if len(sys.argv) > 1 and sys.argv[1].endswith(".so") else OUT
+lib = Path(sys.argv.pop(1)) if len(sys.argv) > 1 and sys.argv[1].endswith((".so", ".o")) else OUT
 for k in kernel_resources(lib):
     if len(sys.argv) > 1 and not any(s in k["name"] for s in sys.argv[1:]):
         continue
