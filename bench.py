@@ -308,6 +308,13 @@ def main():
             if sampled:
                 ev.append((e0, e1))
             return finish(pending.pop(0)) if len(pending) > 1 else None
+        if not wl.get("hess") and not pipelined:  # one rank: sampling inside the baseline launch (2 launches)
+            tx, pb, y = labeler.sample_labels(N_POINTS, on_moments_begin=rec0, on_moments_end=rec1)
+            begun.append((tx, pb))
+            pending.append(("done", y))
+            if sampled:
+                ev.append((e0, e1))
+            return finish(pending.pop(0))
         tx, pb = gen.sample_t_and_x(N_POINTS)
         begun.append((tx, pb))
         if wl.get("hess"):

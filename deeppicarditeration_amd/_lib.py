@@ -61,6 +61,11 @@ SIGNATURES = {
     "dpi_generate_with_gradients": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
                                             c_uint32, c_int, c_float, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),
+    "dpi_sample_with_gradients": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32, c_uint32,
+                                          c_float, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_size_t, c_void_p]),
+    "dpi_sample_points_baseline": (c_int, [c_void_p, c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int,
+                                           c_void_p, c_void_p, c_size_t, c_void_p]),
     "dpi_workspace_bytes_hessians": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_label_moments_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
                                            c_uint32, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

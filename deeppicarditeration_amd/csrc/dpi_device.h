@@ -1027,46 +1027,62 @@ __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh,
 
 // ------------------------------------------------------------------------------ kernels
 // Draws 1-3 (picard/data.py:161-167, equations.py:118-124/:217-230, utils.py:785-789).
+struct SampleSpec {  // k_baseline's in-block sampling of its point (dpi_sample_with_gradients); tx == null: off
+  float* tx;
+  uint32_t k0, k1, c3t, c3x0, c3x, point_base;
+  float eps, alpha_init_sqrt;
+  int t_factors;
+};
+__device__ __forceinline__ float sample_point_t(const EqDev& e, const SampleSpec& s, uint32_t ig) {
+  if (s.t_factors == 0) {  // sample_t_always_uniform (data.py:161-167)
+    const float U = u01_co(philox4x32_10(0u, 0u, ig, s.c3t, s.k0, s.k1).x);
+    return (e.T - 2.f * s.eps) * (1.f - U) + s.eps;
+  }
+  // sample_t (data.py:149-159): T (1 - prod of t_factors uniforms), left to right
+  float prod = 1.f;
+  for (int r0 = 0; r0 < s.t_factors; r0 += 4) {
+    const auto w = philox4x32_10((uint32_t)(r0 >> 2), 0u, ig, s.c3t, s.k0, s.k1);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    for (int q = 0; q < 4 && r0 + q < s.t_factors; ++q) prod *= u01_co(ws[q]);
+  }
+  return e.T * (1.f - prod);
+}
+// x dims 4 j .. 4 j + 3 of point ig at time t
 template <int KIND>
-__global__ void k_sample_points(EqDev e, int n, uint32_t k0, uint32_t k1, uint32_t c3t, uint32_t c3x0,
-                                uint32_t c3x, uint32_t point_base, float eps, int t_factors, float alpha_init_sqrt,
-                                float* tx) {
+__device__ __forceinline__ void sample_point_x4(const EqDev& e, const SampleSpec& s, uint32_t ig, int j, float t,
+                                                float (&x)[4]) {
+  const f4 z = normals4(philox4x32_10((uint32_t)j, 0u, ig, s.c3x, s.k0, s.k1));
+  f4 z0 = {0.f, 0.f, 0.f, 0.f};
+  if (KIND == DPI_EQ_OU) {
+    z0 = normals4(philox4x32_10((uint32_t)j, 0u, ig, s.c3x0, s.k0, s.k1));
+    z0.a *= s.alpha_init_sqrt;
+    z0.b *= s.alpha_init_sqrt;
+    z0.c *= s.alpha_init_sqrt;
+    z0.d *= s.alpha_init_sqrt;
+  }
+  const float sc = sqrtf(t) * e.asq;
+  x[0] = fmaf(sc, z.a, z0.a);
+  x[1] = fmaf(sc, z.b, z0.b);
+  x[2] = fmaf(sc, z.c, z0.c);
+  x[3] = fmaf(sc, z.d, z0.d);
+}
+
+template <int KIND>
+__global__ void k_sample_points(EqDev e, int n, SampleSpec s) {
   const int nb = (e.nx + 3) >> 2;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = gid / nb, j = gid - i * nb;
   if (i >= n) return;
-  const uint32_t ig = point_base + (uint32_t)i;
-  float t;
-  if (t_factors == 0) {  // sample_t_always_uniform (data.py:161-167)
-    const float U = u01_co(philox4x32_10(0u, 0u, ig, c3t, k0, k1).x);
-    t = (e.T - 2.f * eps) * (1.f - U) + eps;
-  } else {  // sample_t (data.py:149-159): T (1 - prod of t_factors uniforms), left to right
-    float prod = 1.f;
-    for (int r0 = 0; r0 < t_factors; r0 += 4) {
-      const auto w = philox4x32_10((uint32_t)(r0 >> 2), 0u, ig, c3t, k0, k1);
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-      for (int q = 0; q < 4 && r0 + q < t_factors; ++q) prod *= u01_co(ws[q]);
-    }
-    t = e.T * (1.f - prod);
-  }
-  float* row = tx + (size_t)i * (1 + e.nx);
+  const uint32_t ig = s.point_base + (uint32_t)i;
+  const float t = sample_point_t(e, s, ig);
+  float* row = s.tx + (size_t)i * (1 + e.nx);
   if (j == 0) row[0] = t;
-  const f4 z = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x, k0, k1));
-  f4 z0 = {0.f, 0.f, 0.f, 0.f};
-  if (KIND == DPI_EQ_OU) {
-    z0 = normals4(philox4x32_10((uint32_t)j, 0u, ig, c3x0, k0, k1));
-    z0.a *= alpha_init_sqrt;
-    z0.b *= alpha_init_sqrt;
-    z0.c *= alpha_init_sqrt;
-    z0.d *= alpha_init_sqrt;
-  }
-  const float sc = sqrtf(t) * e.asq;
-  const float zz[4] = {z.a, z.b, z.c, z.d};
-  const float xx[4] = {z0.a, z0.b, z0.c, z0.d};
+  float x[4];
+  sample_point_x4<KIND>(e, s, ig, j, t, x);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int d = 4 * j + q;
-    if (d < e.nx) row[1 + d] = fmaf(sc, zz[q], xx[q]);
+    if (d < e.nx) row[1 + d] = x[q];
   }
 }
 
@@ -1094,20 +1110,50 @@ __device__ __forceinline__ float block_sum_b(float v, float* red) {
 // f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
 // f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
 // over k-slices (weights read coalesced through the transposed copies), no LDS staging.
+// smp.tx != null: the block first samples its point (draws 1-3, k_sample_points' arithmetic) into
+// smp.tx and its LDS copy, so sample_with_gradients needs no sampling launch; tickets != null: zero
+// this point's ticket of the fused label reduce (k_paths' last-block reduce).
 template <int KIND, bool ZERO>
 __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
                                                   float* __restrict__ gx, float* __restrict__ fb,
-                                                  float* __restrict__ bx, float* __restrict__ hb) {
+                                                  float* __restrict__ bx, float* __restrict__ hb, SampleSpec smp,
+                                                  int* __restrict__ tickets) {
   __shared__ float xs[NXP_MAX];
   __shared__ float act[4][HMAX];
   __shared__ float dbuf[2][HMAX];
   __shared__ float red[NTHB / 64];
+  __shared__ float ts;
   const int i = blockIdx.x, tid = threadIdx.x;
   const int nx = e.nx, F = 1 + nx;
-  const float* row = tx + (size_t)i * F;
-  const float t = row[0];
-  for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
+  if (tickets && tid == 0) tickets[i] = 0;
+  if (smp.tx) {
+    const uint32_t ig = smp.point_base + (uint32_t)i;
+    const int nb = (nx + 3) >> 2;
+    float* row = smp.tx + (size_t)i * F;
+    if (tid < nb) {
+      const float tt = sample_point_t(e, smp, ig);
+      if (tid == 0) {
+        row[0] = tt;
+        ts = tt;
+      }
+      float x[4];
+      sample_point_x4<KIND>(e, smp, ig, tid, tt, x);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * tid + q;
+        if (d < nx) row[1 + d] = x[q];
+        xs[d] = d < nx ? x[q] : 0.f;
+      }
+    } else if (4 * nb <= tid && tid < NXP_MAX) {
+      xs[tid] = 0.f;
+    }
+  } else {
+    const float* row = tx + (size_t)i * F;
+    if (tid == 0) ts = row[0];
+    for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
+  }
   __syncthreads();
+  const float t = ts;
   // g(x): per-thread dims, then per-statistic block sums in fixed order (one barrier pair)
   {
     __shared__ float redn[NTHB / 64][NSG];
@@ -1330,6 +1376,15 @@ struct PathArgs {
   // DATA.ESTIMATE_DELTA_T (data.py:1209-1213): > 0 selects the TD estimators (k_paths<.., TD>),
   // horizon t_next = min(t + td_dt, T), terminal value u(t_next, X) where t_next < T
   float td_dt;
+  // fused label reduce (tickets != null; first-order labels, nbp <= 64): the last block of a point
+  // reduces its nbp slab rows in k_reduce's canonical tree and writes moments / labels (rd_*: the
+  // arguments k_reduce would take)
+  int* tickets;
+  float* rd_moments;
+  float* rd_y;
+  int* rd_status;
+  float rd_invM, rd_bound;
+  int rd_add_g;
 };
 
 // ------------------------------------------------------------------------------ Hessian labels
@@ -1518,6 +1573,61 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
 // T - t below becomes the horizon t_next - t, and where t_next = t + dt < T (workgroup-uniform:
 // one point per workgroup) the terminal value is u(t_next, X_{t_next}), evaluated by the same MLP
 // tile on the terminal noise before the integral rollout takes the noise tile.
+// The label reduce of one point inside k_paths (a.tickets != null; nbp <= 64), replacing the
+// k_reduce launch: every block publishes its slab row (each storing wave waits for its stores, a
+// workgroup barrier, one lane's agent-scope release, then an agent-scope add to the point's
+// ticket — MI355X_MICROARCH.md's producer form); the block whose add returns nbp - 1 acquires
+// (agent scope) and reduces the point's nbp rows, one thread per column over the 64 zero-padded
+// leaves as a perfect binary tree in block order — for nbp <= 64 exactly tree_sum's order, so the
+// moments and labels are bitwise k_reduce's — then finalizes (/M, + g(x), clip) and zeroes the
+// ticket for the next call (k_baseline zeroes it too).
+__device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, const float* out) {
+  __shared__ int last;
+  (void)out;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores complete
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(a.tickets + i, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int is_last = prev == a.nbp - 1;
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last = is_last;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int R = slab_row(F), nbp = a.nbp;
+  const float* base = a.partial + (size_t)i * nbp * R;
+  for (int c = threadIdx.x; c < 2 * F; c += NTH) {
+    // the 64-leaf tree as four 16-leaf subtrees, (q0 + q1) + (q2 + q3): the same additions in the
+    // same order, a quarter of the live registers (the tail runs inside the path kernel)
+    float q[4];
+#pragma unroll 1
+    for (int h = 0; h < 4; ++h) {
+      float v[16];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) v[b] = 16 * h + b < nbp ? base[(size_t)(16 * h + b) * R + c] : 0.f;
+#pragma unroll
+      for (int w = 1; w < 16; w <<= 1)
+#pragma unroll
+        for (int b = 0; b < 16; b += 2 * w) v[b] = v[b] + v[b + w];
+      q[h] = v[0];
+    }
+    const float sum = (q[0] + q[1]) + (q[2] + q[3]);
+    if (c < F && a.rd_status && !__builtin_isfinite(sum)) *(volatile int*)a.rd_status = DPI_STATUS_NONFINITE;
+    a.rd_moments[(size_t)i * 2 * F + c] = sum;
+    if (a.rd_y && c < F) {
+      float y = sum * a.rd_invM;
+      if (c == 0 && a.rd_add_g) y += a.gx[i];
+      a.rd_y[(size_t)i * F + c] = y != y ? y : fminf(fmaxf(y, -a.rd_bound), a.rd_bound);  // torch.clip
+    }
+  }
+  if (threadIdx.x == 0) a.tickets[i] = 0;
+}
+
 template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false>
 __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
@@ -1908,7 +2018,11 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       }
     }
   }
-  if constexpr (HESS) hess_block<KIND, H, L, ZERO, SPLIT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
+  if constexpr (HESS) {
+    hess_block<KIND, H, L, ZERO, SPLIT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
+  } else {
+    if (a.tickets) fused_reduce(a, i, F, out);
+  }
 }
 
 }  // namespace dpi

@@ -34,6 +34,8 @@ struct Launch {
   hipStream_t st;
   bool hess = false;  // k_paths in Hessian-label mode (GBM only)
   bool td = false;    // k_paths with the TD estimators (problem td_dt > 0)
+  SampleSpec smp{};   // baseline: sample the points in the same launch (smp.tx != null)
+  int* tickets = nullptr;  // baseline: zero the fused reduce's per-point tickets
 };
 
 // TDV: the TD-estimator k_paths variants, compiled in translation units of their own
@@ -55,7 +57,7 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
     }
   } else if (q.baseline)
     hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
-                       q.bx, q.hb);
+                       q.bx, q.hb, q.smp, q.tickets);
   else if (q.hess) {
     if constexpr (KIND == DPI_EQ_GBM) {
       EqDev e2 = p->e;

@@ -840,7 +840,7 @@ static int pis_chunk_wg() {
 
 // Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | [PIS rows] | partial[n][2F][nbp]  (256-B aligned)
 struct WsLayout {
-  size_t gx, fb, bx, hb, rows, partial, rq, total;
+  size_t gx, fb, bx, hb, tk, rows, partial, rq, total;
   int rows_cap;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -852,7 +852,8 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   w.fb = al256((size_t)n * 4);
   w.bx = w.fb + al256((size_t)n * 4);
   w.hb = w.bx + al256((size_t)n * H * 4);
-  w.rows = w.hb + al256((size_t)n * NXP_MAX * 4);
+  w.tk = w.hb + al256((size_t)n * NXP_MAX * 4);  // the fused reduce's per-point tickets (k_paths)
+  w.rows = w.tk + al256((size_t)n * 4);
   w.rows_cap = 0;
   size_t rows_bytes = 0;
   if (net && net->d.kind == 2) {
@@ -1106,6 +1107,23 @@ extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) 
   return ws_layout(net, n, M, 1 + p->e.nx).total;
 }
 
+// the counters of draws 1-3 (k_sample_points, k_baseline's in-block sampling)
+static SampleSpec sample_spec(dpi_problem p, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
+                              int t_factors, float* tx) {
+  SampleSpec s;
+  s.tx = tx;
+  s.k0 = (uint32_t)seed;
+  s.k1 = (uint32_t)(seed >> 32);
+  s.c3t = DPI_TAG_T | (epoch << 8);
+  s.c3x0 = DPI_TAG_X0 | (epoch << 8);
+  s.c3x = DPI_TAG_X | (epoch << 8);
+  s.point_base = point_base;
+  s.eps = eps;
+  s.alpha_init_sqrt = p->alpha_init_sqrt;
+  s.t_factors = t_factors;
+  return s;
+}
+
 extern "C" int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
                       float* tx, void* stream) {
   return dpi_sample_points_t(p, n, seed, epoch, point_base, eps, 0, tx, stream);
@@ -1118,22 +1136,18 @@ extern "C" int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t
   if (n == 0) return 0;
   const int nb = (p->e.nx + 3) >> 2;
   const int total = n * nb;
-  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-  const uint32_t c3t = DPI_TAG_T | (epoch << 8), c3x0 = DPI_TAG_X0 | (epoch << 8), c3x = DPI_TAG_X | (epoch << 8);
+  const SampleSpec s = sample_spec(p, seed, epoch, point_base, eps, t_factors, tx);
   dim3 grid((total + 255) / 256), block(256);
   hipStream_t st = (hipStream_t)stream;
   switch (p->e.kind) {
     case DPI_EQ_CHA:
-      hipLaunchKernelGGL(k_sample_points<DPI_EQ_CHA>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, t_factors, p->alpha_init_sqrt, tx);
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_CHA>, grid, block, 0, st, p->e, n, s);
       break;
     case DPI_EQ_OU:
-      hipLaunchKernelGGL(k_sample_points<DPI_EQ_OU>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, t_factors, p->alpha_init_sqrt, tx);
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_OU>, grid, block, 0, st, p->e, n, s);
       break;
     case DPI_EQ_GBM:
-      hipLaunchKernelGGL(k_sample_points<DPI_EQ_GBM>, grid, block, 0, st, p->e, n, k0, k1, c3t, c3x0, c3x, point_base,
-                         eps, t_factors, p->alpha_init_sqrt, tx);
+      hipLaunchKernelGGL(k_sample_points<DPI_EQ_GBM>, grid, block, 0, st, p->e, n, s);
       break;
     default:
       return fail(DPI_ERR_UNSUPPORTED, "sample_points: equation kind");
@@ -1179,7 +1193,7 @@ static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, cons
   // per-point f_b = f(t, x, u, grad u) needs the whole PISGradNet chain, so its n rows ride in the
   // first path chunk's chain (pis_paths) instead of a separate 15-launch chain over n rows
   hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTHB), 0, st, p->e, net->d, tx, n,
-                     (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb));
+                     (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), SampleSpec{}, nullptr);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1332,9 +1346,17 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   if (net->d.kind == 2) return pis_baseline(p, net, tx, n, w, b, (hipStream_t)stream);
   Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), nullptr, 0,
            (hipStream_t)stream};
+  q.tickets = (int*)(b + w.tk);
   if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "point_baseline: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+// The label reduce inside k_paths (fused_reduce) for first-order labels with <= 64 path blocks per
+// point: one launch fewer per label call.  DPI_FUSED_REDUCE=0 keeps the separate k_reduce launch.
+static bool fused_reduce_on() {  // read per call, so one process can compare both
+  const char* e = std::getenv("DPI_FUSED_REDUCE");
+  return !e || std::atoi(e) != 0;
 }
 
 // k_paths phase order policy (see the kernel); DPI_ORDER overrides for ablations.
@@ -1404,13 +1426,79 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
+    if (nbp <= 64 && fused_reduce_on()) {  // k_paths' last block per point reduces and finalizes
+      a.tickets = (int*)(b + w.tk);
+      a.rd_moments = moments;
+      a.rd_y = y;
+      a.rd_status = net_status(net);
+      a.rd_invM = 1.0f / (float)M;
+      a.rd_bound = bound;
+      a.rd_add_g = (flags & DPI_TERMINAL) ? 1 : 0;
+    }
     if (!dispatch_any(p, net, q))
       return fail(DPI_ERR_UNSUPPORTED, "label_moments: unsupported equation/network shape");
+    if (a.tickets) {
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
   }
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, partial, n, F, nbp, moments,
                      (const float*)(b + w.gx), 1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F,
                      net_status(net));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// sample_with_gradients (picard/data.py:211-223) as one call: the points' draws 1-3 inside the
+// baseline launch (k_baseline with SampleSpec), then the fused rollout / label kernel whose last
+// block per point reduces and finalizes — two launches for first-order MLP / zero-net labels.
+// PISGradNet: dpi_sample_points_t + dpi_generate_with_gradients.
+int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, uint64_t seed, uint32_t epoch,
+                              uint32_t point_base, float eps, int t_factors, int flags, float sample_bound, float* tx,
+                              float* y, float* moments, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (n < 0 || M < 1 || K < 1 || epoch > 0xFFFFFFu || t_factors < 0 || t_factors > 4096)
+    return fail(DPI_ERR_ARG, "sample_with_gradients: bad arguments (n >= 0, M, K >= 1, t_factors in [0, 4096])");
+  if (n == 0) return 0;
+  if (!tx || !y || !moments) return fail(DPI_ERR_ARG, "sample_with_gradients: null tx, y or moments");
+  const int F = 1 + p->e.nx;
+  const WsLayout w = ws_layout(net, n, M, F);
+  if (!ws || ws_bytes < w.total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  if (net->d.kind == 2) {
+    if ((rc = dpi_sample_points_t(p, n, seed, epoch, point_base, eps, t_factors, tx, stream))) return rc;
+    return dpi_generate_with_gradients(p, net, tx, n, M, K, seed, epoch, point_base, flags, sample_bound, y, moments, ws,
+                                       ws_bytes, stream);
+  }
+  if ((rc = dpi_sample_points_baseline(p, net, n, seed, epoch, point_base, eps, t_factors, tx, ws, ws_bytes, stream)))
+    return rc;
+  return moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, moments, ws, ws_bytes, stream, y,
+                      sample_bound);
+}
+
+// The points (dpi_sample_points_t's draws) and their baseline (dpi_point_baseline) in ONE launch
+// for MLP / zero networks: each baseline workgroup samples its own point first.
+int dpi_sample_points_baseline(dpi_problem p, dpi_net net, int n, uint64_t seed, uint32_t epoch, uint32_t point_base,
+                               float eps, int t_factors, float* tx, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_pair(p, net);
+  if (rc) return rc;
+  if (n < 0 || (n && (!tx || !ws)) || epoch > 0xFFFFFFu || t_factors < 0 || t_factors > 4096)
+    return fail(DPI_ERR_ARG, "sample_points_baseline: bad arguments (t_factors in [0, 4096])");
+  if (n == 0) return 0;
+  if (net->d.kind == 2) {
+    if ((rc = dpi_sample_points_t(p, n, seed, epoch, point_base, eps, t_factors, tx, stream))) return rc;
+    return dpi_point_baseline(p, net, tx, n, ws, ws_bytes, stream);
+  }
+  const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
+  if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  char* b = (char*)ws;
+  Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), nullptr, 0,
+           (hipStream_t)stream};
+  q.smp = sample_spec(p, seed, epoch, point_base, eps, t_factors, tx);
+  q.tickets = (int*)(b + w.tk);
+  if (!dispatch_any(p, net, q))
+    return fail(DPI_ERR_UNSUPPORTED, "sample_points_baseline: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -197,9 +197,35 @@ class OnlineDataGenerator:
         return tx.to(self.label_dtype), y.to(self.label_dtype)
 
     def sample_with_gradients(self, n_batch):
-        """data.py:211-223: (tx, clip(u_ux)) with u_ux (n, 1+nx)."""
+        """data.py:211-223: (tx, clip(u_ux)) with u_ux (n, 1+nx).  One C-ABI call where it fits
+        (dpi_sample_with_gradients: the sampling inside the baseline launch, the label reduce
+        inside the path launch); tx and labels are bitwise those of the separate calls."""
+        MT, MI = self.n_estimate_terminal, self.n_estimate_integral
+        if MT == MI and MT <= PATHS_PER_CALL_MAX:
+            pb = self._take_points(n_batch)
+            tx, y = self._guarded(lambda: self.sample_generate(n_batch, pb))
+            return self._out(tx, y)
         tx, pb = self.sample_t_and_x(n_batch)
         return self._out(tx, self._generate(tx, pb, _lib.DPI_BOTH))
+
+    def sample_generate(self, n_batch, point_base, bound=None, on_moments_begin=None, on_moments_end=None):
+        """Points at counters [point_base, point_base + n) and their clipped labels (no range guard):
+        (tx, y) from two launches — dpi_sample_points_baseline (the sampling inside the baseline
+        launch), then dpi_label_moments_finalize (the label reduce inside the path launch);
+        last_moments as _generate.  on_moments_*: called around the second (bench timing)."""
+        n, F, M = n_batch, 1 + self.equation.nx, self.n_estimate_integral
+        tx = torch.empty(n, F, dtype=torch.float32, device=self._device)
+        ws = self._workspace(n, M)
+        self._configure_problem()
+        _lib.check(self.lib.dpi_sample_points_baseline(self.problem, self.net.handle, n, self.seed, self.epoch,
+                                                       point_base, self.eps, self.t_factors, _ptr(tx), _ptr(ws),
+                                                       ws.numel(), _stream(self._device)), "dpi_sample_points_baseline")
+        if on_moments_begin:
+            on_moments_begin()
+        y, self.last_moments = self.label_moments_finalize(tx, point_base, M, _lib.DPI_BOTH, ws, bound)
+        if on_moments_end:
+            on_moments_end()
+        return tx, y
 
     def sample_with_gradients_and_hessians(self, n_batch):
         """data.py:225-237: (tx, clip(u_ux_uxx)) with u_ux_uxx (n, 1 + nx + nx^2)."""

@@ -75,7 +75,8 @@ class ShardedLabeler:
         flag = gen.range_status()
         if self.world > 1:
             import torch.distributed as dist
-            t = torch.tensor([float(flag)], device=y.device if dist.get_backend(self.group) != "gloo" else "cpu")
+            dev = (y[-1] if isinstance(y, tuple) else y).device
+            t = torch.tensor([float(flag)], device=dev if dist.get_backend(self.group) != "gloo" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             flag = int(t.item())
         if not flag:
@@ -280,11 +281,24 @@ class ShardedLabeler:
         return self.gen.finalize(mom, M, flags, ws)
 
     # ------------------------------------------------------------------ batch_data_generator surface
+    def sample_labels(self, n_batch, on_moments_begin=None, on_moments_end=None):
+        """(tx, point_base, labels) for the next n_batch points: for one rank the generator's
+        two-launch dpi_sample_with_gradients (range-guarded like labels()), else sampling + labels()."""
+        gen = self.gen
+        if self.world == 1 and gen.n_estimate_terminal == gen.n_estimate_integral and \
+                gen.n_estimate_integral <= 65536:
+            pb = gen._take_points(n_batch)
+            tx, y = self._guarded(lambda: gen.sample_generate(n_batch, pb, on_moments_begin=on_moments_begin,
+                                                              on_moments_end=on_moments_end))
+            return tx, pb, y
+        tx, pb = gen.sample_t_and_x(n_batch)
+        return tx, pb, self.labels(tx, pb, on_moments_begin=on_moments_begin, on_moments_end=on_moments_end)
+
     def sample_with_gradients(self, n_batch):
         """OnlineDataGenerator.sample_with_gradients with this rank's MC shard: every rank draws the
         same points (same counters) and returns the same (tx, clip(u_ux))."""
-        tx, pb = self.gen.sample_t_and_x(n_batch)
-        return tx, self.labels(tx, pb)
+        tx, _, y = self.sample_labels(n_batch)
+        return tx, y
 
     def sample_with_gradients_and_hessians(self, n_batch):
         tx, pb = self.gen.sample_t_and_x(n_batch)

@@ -24,6 +24,8 @@
  *   dpi_label_moments        picard/data.py:899-926 + :471-527 (+ :1226-1325 get_f) summed over MC paths
  *   dpi_label_finalize       picard/data.py:924-926, :525-526, :222  mean over M, + g(x), clip
  *   dpi_generate_with_gradients  picard/data.py:1208-1218 (baseline + moments + finalize)
+ *   dpi_sample_with_gradients    picard/data.py:211-223 (sample_with_gradients: points + all of the above)
+ *   dpi_sample_points_baseline   picard/data.py:211-217 + :506-518, :918-920 (the points and their baseline)
  *   dpi_moments_reduce       (no reference counterpart: fixed-order combine of per-rank moments)
  *   dpi_generate_with_gradients_and_hessians  picard/data.py:1220-1223 (+ :1153-1201, :823-897, :225-237)
  *   dpi_label_moments_hessians / dpi_label_finalize_hessians  the same, split for MC sharding
@@ -218,6 +220,19 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
                                 uint64_t seed, uint32_t epoch, uint32_t point_base, int flags,
                                 float sample_bound, float* y, float* moments, void* ws, size_t ws_bytes,
                                 void* stream);
+
+/* sample_with_gradients(n): the n points of dpi_sample_points_t (eps, t_factors, point_base as
+ * there) into tx (n, 1+nx), then dpi_generate_with_gradients on them — tx, y and moments bitwise
+ * those of the two separate calls.  MLP and zero networks run it as two launches (the sampling
+ * inside the baseline launch, the label reduce inside the path launch). */
+int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, uint64_t seed, uint32_t epoch,
+                              uint32_t point_base, float eps, int t_factors, int flags, float sample_bound,
+                              float* tx, float* y, float* moments, void* ws, size_t ws_bytes, void* stream);
+
+/* dpi_sample_points_t + dpi_point_baseline (tx and the workspace's baseline bitwise those of the
+ * two calls), one launch for MLP / zero networks: the first half of dpi_sample_with_gradients. */
+int dpi_sample_points_baseline(dpi_problem p, dpi_net net, int n, uint64_t seed, uint32_t epoch, uint32_t point_base,
+                               float eps, int t_factors, float* tx, void* ws, size_t ws_bytes, void* stream);
 
 /* Malliavin-weight Hessian labels: replaces
  *   _OnlineDataGenerator.sample_with_gradients_and_hessians (picard/data.py:225-237, after its

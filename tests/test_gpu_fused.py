@@ -1,0 +1,95 @@
+"""The two-launch sample_with_gradients (round 4): the points sampled inside the baseline launch
+(dpi_sample_points_baseline) and the label reduce inside the path launch (k_paths' last block per
+point, DPI_FUSED_REDUCE) against the separate launches they replace — k_sample_points,
+k_baseline, k_paths, k_reduce — bit for bit (reference picard/data.py:211-223)."""
+import pytest
+import torch
+
+import deeppicarditeration_amd as dpi
+from deeppicarditeration_amd import _lib as L
+from deeppicarditeration_amd.sharding import ShardedLabeler
+
+pytestmark = pytest.mark.gpu
+
+NX = 100
+
+
+def _make(kind, M, K, t_uniform=True, seed=7):
+    torch.manual_seed(0)
+    hess = None
+    if kind == "cha":
+        eq, widths = dpi.Cha(NX, 1.0, 5.0, 1.0), [128] * 4
+    elif kind == "ou":
+        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+        widths = [64, 64]
+    else:
+        eq, widths = dpi.GBMEquationComplexExact(NX, 1.0, 1.0), [64] * 3
+        hess = {"method": "SDGD", "kwargs": {"v": 100}}
+    net = dpi.construct_mlp(1 + NX, 1, widths, ["ELU"] * len(widths), None) if kind != "zero" else dpi.ZeroSolution(1)
+    if kind == "zero":
+        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
+    return dpi.OnlineDataGenerator(eq, net, 10, 3, device="cuda:0", t_always_uniform=t_uniform, n_estimate_terminal=M,
+                                   n_estimate_integral=M, n_euler_steps=K, seed=seed, hessian_approximation=hess)
+
+
+def _separate(gen, n, pb):
+    """k_sample_points, then k_baseline + k_paths + k_reduce (DPI_FUSED_REDUCE=0)."""
+    tx, _ = gen.sample_t_and_x(n, point_base=pb)
+    ws = gen.point_baseline(tx)
+    y, mom = gen.label_moments_finalize(tx, pb, gen.n_estimate_integral, L.DPI_BOTH, ws)
+    return tx, y, mom
+
+
+@pytest.mark.parametrize("kind,n,M,K,t_uniform", [("cha", 16, 4096, 50, True), ("cha", 5, 192, 3, False),
+                                                  ("gbm", 8, 1024, 4, True), ("ou", 3, 128, 4, True),
+                                                  ("zero", 4, 64, 2, True)])
+def test_two_launch_sample_with_gradients_is_bitwise_the_separate_launches(kind, n, M, K, t_uniform, monkeypatch):
+    gen = _make(kind, M, K, t_uniform)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "0")
+    tx0, y0, mom0 = _separate(gen, n, 40)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    tx1, y1 = gen.sample_generate(n, 40)
+    mom1 = gen.last_moments
+    torch.cuda.synchronize()
+    assert torch.equal(tx0, tx1)
+    assert torch.equal(mom0, mom1)
+    assert torch.equal(y0, y1)
+    assert torch.isfinite(y1).all()
+
+
+def test_fused_reduce_repeated_calls_reuse_the_tickets(monkeypatch):
+    """The tickets reset themselves: three calls on one workspace (one baseline) equal fresh ones."""
+    gen = _make("cha", 1024, 2)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    tx, _ = gen.sample_t_and_x(6, point_base=3)
+    ws = gen.point_baseline(tx)
+    outs = [gen.label_moments_finalize(tx, 3, 1024, L.DPI_BOTH, ws)[0] for _ in range(3)]
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "0")
+    ref = gen.label_moments_finalize(tx, 3, 1024, L.DPI_BOTH, ws)[0]
+    for y in outs:
+        assert torch.equal(y, ref)
+
+
+def test_sharded_moments_with_the_fused_reduce_equal_the_single_call(monkeypatch):
+    """Two MC shards of 2048 paths (32 blocks each, fused reduce) combined by the rank tree equal one
+    4096-path call (64 blocks) bit for bit."""
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    gen = _make("cha", 4096, 3)
+    tx, pb = gen.sample_t_and_x(4, point_base=0)
+    ws = gen.point_baseline(tx)
+    parts = torch.stack([gen.label_moments(tx, pb, 4096, r * 2048, (r + 1) * 2048, L.DPI_BOTH, ws) for r in range(2)])
+    two = gen.moments_reduce(parts)
+    one = gen.label_moments(tx, pb, 4096, 0, 4096, L.DPI_BOTH, ws)
+    assert torch.equal(one, two)
+
+
+def test_generator_and_labeler_surfaces_use_the_two_launch_path():
+    """sample_with_gradients of the generator and of a one-rank ShardedLabeler: same points, same
+    labels as the separate launches."""
+    a, b, c = _make("cha", 512, 3), _make("cha", 512, 3), _make("cha", 512, 3)
+    tx_a, y_a = a.sample_with_gradients(8)
+    tx_b, y_b = ShardedLabeler(b).sample_with_gradients(8)
+    tx_c, y_c, _ = _separate(c, 8, 0)
+    assert torch.equal(tx_a, tx_c) and torch.equal(tx_b, tx_c)
+    assert torch.equal(y_a, y_c) and torch.equal(y_b, y_c)
