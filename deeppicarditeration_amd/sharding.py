@@ -285,8 +285,8 @@ class ShardedLabeler:
         """(tx, point_base, labels) for the next n_batch points: for one rank the generator's
         two-launch dpi_sample_with_gradients (range-guarded like labels()), else sampling + labels()."""
         gen = self.gen
-        if self.world == 1 and gen.n_estimate_terminal == gen.n_estimate_integral and \
-                gen.n_estimate_integral <= 65536:
+        if self.world == 1 and hasattr(gen, "sample_generate") and \
+                gen.n_estimate_terminal == gen.n_estimate_integral and gen.n_estimate_integral <= 65536:
             pb = gen._take_points(n_batch)
             tx, y = self._guarded(lambda: gen.sample_generate(n_batch, pb, on_moments_begin=on_moments_begin,
                                                               on_moments_end=on_moments_end))
