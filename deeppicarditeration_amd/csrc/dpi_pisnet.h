@@ -186,8 +186,9 @@ enum { PN_ELU = 0, PN_DELU_LDS = 1, PN_DELU_HBM = 2 };
 
 // Row traffic (IN, the saved activations, GX) goes through a buffer resource based at the block's
 // first row and sized to its valid rows: rows past R read as zeros and their stores are dropped, so
-// the partial last tile needs no clamped addresses, and every access is one 32-bit lane offset plus
-// a wave-uniform scalar offset (no 64-bit per-lane pointers held across the layers).  NTS: the
+// the partial last tile needs no clamped addresses, and every access is one 32-bit lane offset
+// (holding the whole row offset: the range check ignores the scalar offset) plus a wave-uniform
+// scalar offset for the columns (no 64-bit per-lane pointers held across the layers).  NTS: the
 // non-temporal hint (cache policy nt), so the row streams through L2 do not evict the chain's
 // weights (7 MB, shared by every block of the XCD).
 template <bool NTS>
@@ -231,8 +232,17 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
   const int vrow = gr * ldb + 16 * gg;                        // + scalar 4 (reg + 32 c)
   auto gdst = [&](uint32_t* slab) { return reinterpret_cast<u32x4_t*>(slab + gr * 32 + 4 * (gg ^ x3_swz(gr))); };
   // a lane's own granule pairs of the 512-wide regions: row 16 b + il, chunk 2 wv + c, pair ql
-  const int vown = il * ldb + 32 * ql;                        // + scalar 16 b ldb + 4 reg + 128 (2 wv + c)
-  auto sown = [&](int reg, int b, int c) { return 16 * b * ldb + 4 * reg + 128 * (2 * wv + c); };
+  // A buffer instruction's range check covers the VGPR (+ immediate) offset but not the scalar one,
+  // so a row past R must be past num_records in the VGPR part alone: with 16 b ldb in the scalar
+  // offset, rows 16 b + il >= mrows of a partial tile with il < mrows would pass the check and land
+  // past the chunk's rows.  The scalar offset carries only the region and chunk columns (< a row).
+  // So path tile b gets a resource of its own, based at its row 16 b and sized to its valid rows
+  // (scalar registers only), and the lane offset il ldb + 32 ql is the same for every tile.
+  const int vown = il * ldb + 32 * ql;                        // + scalar 4 reg + 128 (2 wv + c)
+  auto rown = [&](int b) {
+    return pn_rsrc(rbase + (size_t)(16 * b) * L.stride, (size_t)max(0, mrows - 16 * b) * ldb);
+  };
+  auto sown = [&](int reg, int c) { return 4 * reg + 128 * (2 * wv + c); };
 
   // the 512-wide products: wave wv owns units 64 wv .. 64 wv + 63 (4 unit tiles) of all 64 rows
   pn_f4 acc[4][4];
@@ -310,8 +320,8 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
         u32x4_t eh, el;
         pn_split8(v, eh, el);
         if (save_reg >= 0) {  // rows past R: dropped by the buffer's range check
-          pn_st<NTS>(rr, vown, sown(save_reg, b, c), eh);
-          pn_st<NTS>(rr, vown, sown(save_reg, b, c) + 16, el);
+          pn_st<NTS>(rown(b), vown, sown(save_reg, c), eh);
+          pn_st<NTS>(rown(b), vown, sown(save_reg, c) + 16, el);
         }
         *lds_at(b, c, 0) = eh;
         *lds_at(b, c, 1) = el;
@@ -374,8 +384,8 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        xh[b][c] = pn_ld<NTS>(rr, vown, sown(L.A[l - 1], b, c));
-        xl[b][c] = pn_ld<NTS>(rr, vown, sown(L.A[l - 1], b, c) + 16);
+        xh[b][c] = pn_ld<NTS>(rown(b), vown, sown(L.A[l - 1], c));
+        xl[b][c] = pn_ld<NTS>(rown(b), vown, sown(L.A[l - 1], c) + 16);
       }
     if (l > 1)
       pre_vjp(l - 1);
