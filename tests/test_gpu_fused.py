@@ -93,3 +93,32 @@ def test_generator_and_labeler_surfaces_use_the_two_launch_path():
     tx_c, y_c, _ = _separate(c, 8, 0)
     assert torch.equal(tx_a, tx_c) and torch.equal(tx_b, tx_c)
     assert torch.equal(y_a, y_c) and torch.equal(y_b, y_c)
+
+
+@pytest.mark.parametrize("kind", ["pis", "cha"])
+def test_label_calls_write_nothing_past_the_workspace(kind):
+    """A partial last tile (3 points x 64 paths = 192 rows: one full 128-row tile and a half one)
+    must not store past the workspace:
+    a canary of 4 MB after dpi_workspace_bytes stays untouched (k_pis_net's row saves go through
+    per-tile buffer resources whose range check covers the whole row offset)."""
+    torch.manual_seed(0)
+    if kind == "pis":
+        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+        net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=NX, g0=eq.g, T=1.0)
+    else:
+        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
+        net = dpi.construct_mlp(1 + NX, 1, [128] * 4, ["ELU"] * 4, None)
+    n, M = 3, 64
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
+                                  n_estimate_integral=M, n_euler_steps=4, seed=5)
+    need = gen.workspace_bytes(n, M)
+    canary = 4 << 20
+    buf = torch.full((need + canary,), 0xA5, dtype=torch.uint8, device="cuda:0")
+    ws = buf[:need]
+    tx, pb = gen.sample_t_and_x(n, point_base=0)
+    gen.point_baseline(tx, ws=ws)
+    mom = gen.label_moments(tx, pb, M, 0, M, L.DPI_BOTH, ws)
+    torch.cuda.synchronize()
+    assert torch.isfinite(mom).all()
+    assert bool((buf[need:] == 0xA5).all())
