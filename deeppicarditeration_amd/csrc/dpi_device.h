@@ -624,6 +624,10 @@ struct LdsGbm {
   float tau[P], cmul[P], bsh[P], fbp[P];
   float smt[P];                    // Hessian labels: s - t per path
   unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
+  // SDGD: each path's distinct sampled directions in increasing order (mlp_hdiag_split's sweep)
+  static constexpr int DLCAP = 96;
+  unsigned char dl[P * DLCAP];
+  unsigned char nd[P];
 };
 
 __device__ __forceinline__ float d2elu_from_a(float a) { return a > 0.f ? 0.f : a + 1.0f; }
@@ -926,8 +930,8 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int r = 0; r < 4; ++r) zz[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
   };
-  // one direction: z (in) is clobbered; zn receives z_0 of direction dn
-  auto direction = [&](int d, float (&z)[HT][4], float (&zn)[HT][4], int dn) {
+  // one direction: z (in) is clobbered; zn receives z_0 of direction dn; counted: weight cnt (else 0)
+  auto direction = [&](int d, float (&z)[HT][4], float (&zn)[HT][4], int dn, bool counted) {
     f32x2 term2 = {0.f, 0.f};
     auto acc_terms = [&](const float (&lm)[HT][4], const float (&zz)[HT][4]) {
 #pragma unroll
@@ -953,18 +957,62 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       acc_terms(lam[l], z);
     }
     const float ud = qsum(term2.x + term2.y);
-    const float c = (float)sh.cnt[d * P + pp];
+    const float c = counted ? (float)sh.cnt[d * P + pp] : 0.f;
     s1 = fmaf(c, ud, s1);
     s2 = fmaf(c, fabsf(ud), s2);
   };
   float za[HT][4], zb[HT][4];
-  ldz(0, za);
-  int d = 0;
-  for (; d + 1 < e.nx; d += 2) {
-    direction(d, za, zb, d + 1);
-    direction(d + 1, zb, za, d + 2 < e.nx ? d + 2 : d + 1);
+  // SDGD (v draws with replacement, data.py:497-502) leaves about 37 % of the directions of a path
+  // unsampled (count 0): the sweep then runs over each path's own distinct directions, in
+  // increasing order — the MFMA batch of 16 paths needs no common direction, only per-lane
+  // z_0 = W1x[:, d_p] — for max over the wave's paths of their distinct counts (about 70 of 100 at
+  // v = nx = 100).  A path's padding slots repeat its last direction with weight 0, which leaves
+  // s1, s2 exactly as the full sweep's fmaf(0, u_dd, s) steps do: the labels are bitwise the
+  // full sweep's.  The exact diagonal (sdgd_v = 0) and paths with more than DLCAP distinct
+  // directions take the full sweep.
+  int ndp = e.nx, kmax = e.nx;
+  bool lists = false;
+  if (e.sdgd_v > 0) {
+    constexpr int DLCAP = LdsGbm<H>::DLCAP;
+    if (qq == 0) {
+      int k = 0;
+      for (int dd = 0; dd < e.nx; ++dd)
+        if (sh.cnt[dd * P + pp]) {
+          if (k < DLCAP) sh.dl[pp * DLCAP + k] = (unsigned char)dd;
+          ++k;
+        }
+      sh.nd[pp] = (unsigned char)min(k, 255);
+    }
+    // the list of path pp is written by its lane qq = 0 and read by the path's four lanes: LDS
+    // operations of one wave complete in order; the asm keeps the compiler from hoisting the reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ndp = sh.nd[pp];
+    kmax = ndp;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
+    lists = kmax <= DLCAP;
   }
-  if (d < e.nx) direction(d, za, zb, d);
+  if (lists) {
+    constexpr int DLCAP = LdsGbm<H>::DLCAP;
+    auto dir = [&](int k) { return (int)sh.dl[pp * DLCAP + min(k, ndp - 1)]; };
+    int k = 0, dk = dir(0);
+    ldz(dk, za);
+    for (; k + 1 < kmax; k += 2) {
+      const int d1 = dir(k + 1), d2 = dir(k + 2);
+      direction(dk, za, zb, d1, k < ndp);
+      direction(d1, zb, za, d2, k + 1 < ndp);
+      dk = d2;
+    }
+    if (k < kmax) direction(dk, za, zb, dk, k < ndp);
+  } else {
+    ldz(0, za);
+    int d = 0;
+    for (; d + 1 < e.nx; d += 2) {
+      direction(d, za, zb, d + 1, true);
+      direction(d + 1, zb, za, d + 2 < e.nx ? d + 2 : d + 1, true);
+    }
+    if (d < e.nx) direction(d, za, zb, d, true);
+  }
   s1_out = s1;
   s2_out = s2;
 }

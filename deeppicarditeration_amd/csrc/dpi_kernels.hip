@@ -685,18 +685,19 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
       align();
       const float *w0 = nnw[0], *wl = nnw[L];
       const int in0 = ins[0], h0 = hidden[0], inl = ins[L];
-      s_gxno = pack_split_x3(blob, NOP, hp[0] + hp[L - 1], [&](int d, int k) {
+      // K order [A_{L-1} | D_0]: k_pis_net forms the A_{L-1} half while A_{L-1} is still in LDS
+      s_gxno = pack_split_x3(blob, NOP, hp[L - 1] + hp[0], [&](int d, int k) {
         if (d >= nx) return 0.f;
-        if (k < hp[0]) return k < h0 ? w0[(size_t)k * in0 + C + d] : 0.f;
-        k -= hp[0];
-        return k < inl ? wl[(size_t)d * inl + k] : 0.f;
+        if (k < hp[L - 1]) return k < inl ? wl[(size_t)d * inl + k] : 0.f;
+        k -= hp[L - 1];
+        return k < h0 ? w0[(size_t)k * in0 + C + d] : 0.f;
       }, &w_gxno);
     }
     for (int l = 0; l <= L; ++l) {
       s_nnF[l] = pack_frag_major(blob, s_nn[l], l < L ? hp[l] : NOP, l == 0 ? INP : hp[l - 1]);
       s_nnTF[l] = pack_frag_major(blob, s_nnT[l], l == 0 ? NOP : hp[l - 1], l == 0 ? hp[0] : l == L ? NXK : hp[l]);
     }
-    s_gxnoF = pack_frag_major(blob, s_gxno, NOP, hp[0] + hp[L - 1]);
+    s_gxnoF = pack_frag_major(blob, s_gxno, NOP, hp[L - 1] + hp[0]);
     for (int l = 0; l <= L; ++l) {
       const int o = l < L ? hidden[l] : nx, op = l < L ? hp[l] : NOP;
       align();
@@ -1055,10 +1056,10 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
             rows + L.A[l - 1], ld, st);
     std::swap(dcur, dnext);
   }
-  // GX = J^T X + net_out = [D_0 | A_{L-1}] . [nnT[0] | nn[L]]^T + b_L: one GEMM with K = h_0 + h_{L-1}
-  // (k_pis_final and k_pis_base_final only need the sum)
-  gemm_x3(EPI_BIAS, R, r64(pd.h[0]) + Kp, NOP, pd.gxnoS, pd.gxnoW, rows + dcur, ld, rows + L.GX, ld, pd.nnbP[pd.L],
-          nullptr, 0, st, rows + L.A[pd.L - 1], ld, r64(pd.h[0]));
+  // GX = net_out + J^T X = [A_{L-1} | D_0] . [nn[L] | nnT[0]]^T + b_L: one GEMM with K = h_{L-1} + h_0,
+  // the A_{L-1} chunks first (k_pis_net's order; k_pis_final and k_pis_base_final only need the sum)
+  gemm_x3(EPI_BIAS, R, Kp + r64(pd.h[0]), NOP, pd.gxnoS, pd.gxnoW, rows + L.A[pd.L - 1], ld, rows + L.GX, ld,
+          pd.nnbP[pd.L], nullptr, 0, st, rows + dcur, ld, Kp);
   return L;
 }
 
@@ -1185,18 +1186,11 @@ static int pis_check(dpi_problem p) {
   return 0;
 }
 
-static int pis_baseline(dpi_problem p, dpi_net net, const float* tx, int n, const WsLayout& w, char* b,
-                        hipStream_t st) {
-  int rc = pis_check(p);
-  if (rc) return rc;
-  // g(x) only (k_baseline's zero-net instance; its f_b placeholder is overwritten by pis_paths): the
-  // per-point f_b = f(t, x, u, grad u) needs the whole PISGradNet chain, so its n rows ride in the
-  // first path chunk's chain (pis_paths) instead of a separate 15-launch chain over n rows
-  hipLaunchKernelGGL((k_baseline<DPI_EQ_OU, true>), dim3(n), dim3(NTHB), 0, st, p->e, net->d, tx, n,
-                     (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), SampleSpec{}, nullptr);
-  HIPCHK(hipGetLastError());
-  return 0;
-}
+// PISGradNet: nothing to launch.  The per-point f_b = f(t, x, u, grad u) needs the whole
+// PISGradNet chain, so its n rows ride in the first path chunk's chain, and g(x) is formed beside it
+// in k_pis_base_final (pis_paths): every label call computes both before k_pis_final and the reduce
+// read them, and the prepare stream's rollout needs neither.
+static int pis_baseline(dpi_problem p) { return pis_check(p); }
 
 // Independent Philox chains per wave in the PISGradNet rollout: 4 (default; 61 VGPRs) or 2
 // (DPI_PIS_UNROLL=2; 47 VGPRs, room beside the 256 x 128 GEMM's blocks).
@@ -1279,7 +1273,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
           (void)hipMemsetAsync(rq, 0, 256 + (size_t)PIS_CLAIM_SLOTS * 4, st);
           hipLaunchKernelGGL((k_pis_rollout_shared<DPI_EQ_OU, true>), dim3(4 * cu_count() * (1 + pis_prep_shared())),
                              dim3(P), 0, st, p->e, net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t,
-                             a.c3s, a.c3i, a.point_base, a.gx, rows, L, stage, dt, 0, 2 * gprep, rq, rq + 64, 1);
+                             a.c3s, a.c3i, a.point_base, rows, L, stage, dt, 0, 2 * gprep, rq, rq + 64, 1);
           return;
         }
       }
@@ -1290,12 +1284,12 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
         const dim3 grid(2 * std::min(step, gend - bx0)), block(P);
         if (pis_rollout_unroll() == 4)
           hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
-                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L,
-                             stage, dt, bx0);
+                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, rows, L, stage,
+                             dt, bx0);
         else
           hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 2>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
-                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, a.gx, rows, L,
-                             stage, dt, bx0);
+                             a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, rows, L, stage,
+                             dt, bx0);
       }
     };
     const bool base = g0 == 0;
@@ -1305,7 +1299,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       if (a.flags & DPI_TERMINAL) {
         const PisRows Lt = chain(false, g * P);
         hipLaunchKernelGGL((k_pis_tvalue<DPI_EQ_OU, X3>), dim3(g), dim3(256), 0, st, p->e, net->pis, tx, g0, a.nbp,
-                           a.gx, rows, Lt, g * P, dt);
+                           rows, Lt, g * P, dt);
       }
       rollout(PIS_TD_INT);
     } else if (!(prepared && base)) {
@@ -1319,9 +1313,9 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
     const PisRows Lc = chain(true, g * P + (base ? n : 0));
     if (base)
       hipLaunchKernelGGL((k_pis_base_final<DPI_EQ_OU, X3>), dim3((n + 63) / 64), dim3(256), 0, st, p->e, net->pis,
-                         brows, Lc, n, fb);
+                         tx, brows, Lc, n, fb, (float*)(b + w.gx));
     hipLaunchKernelGGL((k_pis_final<DPI_EQ_OU, X3>), dim3(g), dim3(NTH), 0, st, p->e, net->pis, tx, g0, a.nbp, K,
-                       a.flags, fb, rows, Lc, a.partial, dt);
+                       a.flags, fb, a.gx, rows, Lc, a.partial, dt);
   };
   for (int g0 = 0; g0 < G; g0 += GC) {
     const int g = std::min(GC, G - g0);
@@ -1343,7 +1337,7 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   const WsLayout w = ws_layout(net, n, 0, 1 + p->e.nx);
   if (ws_bytes < w.partial) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
-  if (net->d.kind == 2) return pis_baseline(p, net, tx, n, w, b, (hipStream_t)stream);
+  if (net->d.kind == 2) return pis_baseline(p);
   Launch q{true, tx, n, (float*)(b + w.gx), (float*)(b + w.fb), (float*)(b + w.bx), (float*)(b + w.hb), nullptr, 0,
            (hipStream_t)stream};
   q.tickets = (int*)(b + w.tk);

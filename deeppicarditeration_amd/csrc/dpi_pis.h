@@ -43,7 +43,7 @@ struct NetPisDev {
   const uint32_t *te0S, *te2S, *sn0S, *snS[4];
   const uint32_t *nnS[5], *nnTS[5];
   const float* nnbP[5];
-  // [nnT[0] | nn[L]] ((nx -> 64) x (h_0 + h_{L-1})): J^T X + net_out = [D_0 | A_{L-1}] . this^T + b_L
+  // [nn[L] | nnT[0]] ((nx -> 64) x (h_{L-1} + h_0)): net_out + J^T X = [A_{L-1} | D_0] . this^T + b_L
   const uint32_t* gxnoS;
   // fragment-major copies for k_pis_net (dpi_pisnet.h): per 16-row tile T and 32-deep chunk c a
   // 2 KB block, the 64 lanes' hi granules (lane l: row 16 T + l % 16, granule pair l / 16) then
@@ -110,9 +110,8 @@ template <int KIND, bool X3, int UNR>
 __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                  uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
-                                                 uint32_t point_base, const float* __restrict__ gx,
-                                                 float* __restrict__ rows, const PisRows& L, int stage, float td_dt,
-                                                 int bx, bool integral) {
+                                                 uint32_t point_base, float* __restrict__ rows, const PisRows& L,
+                                                 int stage, float td_dt, int bx, bool integral) {
   const int lane = threadIdx.x & 63;
   const int g = g0 + bx;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
@@ -167,7 +166,7 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
         for (int j = 0; j < PIS_CH; ++j) pis_embed(pn, pn.T - (t + td_dt), row + L.E, j);
       }
     }
-    row[L.SC + 2] = TERM ? Eq<KIND>::gfin(e, gst) - gx[i] : 0.f;  // a_p = g(X_T) - g(x)
+    row[L.SC + 2] = TERM ? Eq<KIND>::gfin(e, gst) : 0.f;  // g(X_T); k_pis_final forms a_p = g(X_T) - g(x)
     return;
   }
   // integral path
@@ -219,10 +218,10 @@ template <int KIND, bool X3, int UNR = 4>
 __global__ __launch_bounds__(64, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                     int nbp, int m_begin, int K, int flags, uint32_t k0, uint32_t k1,
                                                     uint32_t c3t, uint32_t c3s, uint32_t c3i, uint32_t point_base,
-                                                    const float* __restrict__ gx, float* __restrict__ rows, PisRows L,
-                                                    int stage, float td_dt, int bx0) {
-  pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows,
-                                  L, stage, td_dt, bx0 + (int)(blockIdx.x >> 1), blockIdx.x & 1);
+                                                    float* __restrict__ rows, PisRows L, int stage, float td_dt,
+                                                    int bx0) {
+  pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
+                                  stage, td_dt, bx0 + (int)(blockIdx.x >> 1), blockIdx.x & 1);
 }
 
 // The prepare stream's rollout (dpi_label_prepare), beside the previous batch's k_pis_net: a
@@ -241,8 +240,8 @@ template <int KIND, bool X3, int UNR>
 __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0, int nbp,
                                                             int m_begin, int K, int flags, uint32_t k0,
                                                            uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
-                                                           uint32_t point_base, const float* __restrict__ gx,
-                                                           float* __restrict__ rows, PisRows L, int stage, float td_dt,
+                                                           uint32_t point_base, float* __restrict__ rows, PisRows L,
+                                                           int stage, float td_dt,
                                                            int bx0, int ntask, int* __restrict__ queue,
                                                            int* __restrict__ claim, int waves) {
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);         // HW_REG_HW_ID
@@ -257,18 +256,18 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
     if (lane == 0) t = atomicAdd(queue, 1);
     t = __shfl(t, 0, 64);
     if (t >= ntask) break;
-    pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows,
-                                    L, stage, td_dt, bx0 + (t >> 1), t & 1);
+    pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
+                                    stage, td_dt, bx0 + (t >> 1), t & 1);
   }
 }
 
 #define DPI_PIS_SHARED_ARGS                                                                                         \
   EqDev e, NetPisDev pn, const float *__restrict__ tx, int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,  \
-      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i, uint32_t point_base, const float *__restrict__ gx,      \
-      float *__restrict__ rows, PisRows L, int stage, float td_dt, int bx0, int ntask, int *__restrict__ queue,     \
-      int *__restrict__ claim, int waves
+      uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i, uint32_t point_base, float *__restrict__ rows,         \
+      PisRows L, int stage, float td_dt, int bx0, int ntask, int *__restrict__ queue, int *__restrict__ claim,      \
+      int waves
 #define DPI_PIS_SHARED_CALL \
-  e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, gx, rows, L, stage, td_dt, bx0, ntask, queue, claim, waves
+  e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L, stage, td_dt, bx0, ntask, queue, claim, waves
 // one wave per SIMD: 4 Philox chains per wave, <= 48 registers (beside two 232-register k_pis_net waves)
 template <int KIND, bool X3>
 __global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(24))) void k_pis_rollout_shared(DPI_PIS_SHARED_ARGS) {
@@ -574,11 +573,16 @@ __device__ __forceinline__ void pis_z_stats(const EqDev& e, const NetPisDev& pn,
   smooth_out = smooth;
 }
 
-// Baseline f_b (state part) and nothing else: one 256-thread block per 64 points (4 threads per
-// point; a latency chain, so the GMM staging is spread over all 256 threads).
+// Baseline f_b (state part) and g(x) of the n points: one 256-thread block per 64 points (4
+// threads per point; a latency chain, so the GMM staging is spread over all 256 threads).  g(x) is
+// formed here, inside the label call, rather than by a baseline launch before the rollout: the
+// rollout writes g(X_T) and k_pis_final subtracts g(x), so the prepare stream's rollout of the next
+// batch depends on nothing but its points.  Lane q sums the GMM statistics of dims d = q mod 4 in
+// ascending d, then the quad combines them as (q0 + q1) + (q2 + q3).
 template <int KIND, bool X3>
-__global__ __launch_bounds__(256) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ rows, PisRows L,
-                                                        int n, float* __restrict__ fb) {
+__global__ __launch_bounds__(256) void k_pis_base_final(EqDev e, NetPisDev pn, const float* __restrict__ tx,
+                                                        const float* __restrict__ rows, PisRows L, int n,
+                                                        float* __restrict__ fb, float* __restrict__ gx) {
   __shared__ PisGmmLds gmm;
   __builtin_amdgcn_s_setprio(2);
   pis_stage_gmm(e, gmm);
@@ -589,16 +593,28 @@ __global__ __launch_bounds__(256) void k_pis_base_final(EqDev e, NetPisDev pn, c
   float A, B, sm;
   pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - row[L.SC + 0], q, A, B, sm);
   if (i < n && q == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, A, B);
+  const int nx = e.nx;
+  const float* xr = tx + (size_t)ic * (1 + nx) + 1;
+  float st[NSG];
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) st[c] = 0.f;
+  for (int d = q; d < nx; d += 4) Eq<KIND>::gstat(e, d, xr[d], st);
+#pragma unroll
+  for (int c = 0; c < NSG; ++c) {
+    st[c] += __shfl_xor(st[c], 1, 64);
+    st[c] += __shfl_xor(st[c], 2, 64);
+  }
+  if (i < n && q == 0) gx[i] = Eq<KIND>::gfin(e, st);
 }
 
 // TD terminal value (data.py:941-942): for the rows of points with t + td_dt < T, after the
-// forward chain on (t_next, X_{t_next}) rows, a_p = u(t_next, X) - g(x) with
+// forward chain on (t_next, X_{t_next}) rows, u(t_next, X) into SC + 2 (k_pis_final forms
+// a_p = u - g(x), as it does for the rollout's g(X_T)), with
 // u = smooth (net_out . X) + (1 - smooth) g0(e^{-lambda/2} X), lambda = T - t_next
 // (solution.py:256-289).  4 threads per row.
 template <int KIND, bool X3>
 __global__ void k_pis_tvalue(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0, int nbp,
-                             const float* __restrict__ gx, float* __restrict__ rows, PisRows L, int nrows,
-                             float td_dt) {
+                             float* __restrict__ rows, PisRows L, int nrows, float td_dt) {
   const int r = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
   const int rc = min(r, nrows - 1);
   const int g = g0 + rc / P, i = g / nbp;
@@ -659,15 +675,15 @@ __global__ void k_pis_tvalue(EqDev e, NetPisDev pn, const float* __restrict__ tx
   for (int c = 0; c < NSG; ++c) ws += c < e.ncomp ? __expf(lp[c] - mx) : 0.f;
   const float g0v = -(mx + __logf(ws));  // g0 = -log p (equations.py:592-593)
   const float u = smooth * sp + (1.0f - smooth) * g0v;
-  if (r < nrows && q == 0 && td_u) row[L.SC + 2] = u - gx[i];
+  if (r < nrows && q == 0 && td_u) row[L.SC + 2] = u;
 }
 
 // Per-path f, b_p and label contributions for one (point, 64-path block) -> partial slab.
 template <int KIND, bool X3>
 __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                    int nbp, int K, int flags, const float* __restrict__ fbv,
-                                                   const float* __restrict__ rows, PisRows L,
-                                                   float* __restrict__ partial, float td_dt) {
+                                                   const float* __restrict__ gxv, const float* __restrict__ rows,
+                                                   PisRows L, float* __restrict__ partial, float td_dt) {
   __shared__ float part[4][4][64];  // per-wave 16-path column sums: [wave][q][value]
   __shared__ float vsum[4][2];      // per-wave sums of the value column and its square
   __shared__ PisGmmLds gmm;
@@ -686,7 +702,9 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   const float f_b = fbv[i];
   const int p = tid >> 2, q = tid & 3;
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;
-  const float s = row[L.SC + 0], ap = row[L.SC + 2], smt = row[L.SC + 3];
+  // a_p = g(X_T) - g(x) (TD: u(t_next, X) - g(x) where t_next < T); the terminal wave wrote 0 for
+  // integral-only calls
+  const float s = row[L.SC + 0], ap = TERM ? row[L.SC + 2] - gxv[i] : 0.f, smt = row[L.SC + 3];
   float A, B, sm;
   pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;

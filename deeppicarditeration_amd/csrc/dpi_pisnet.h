@@ -6,11 +6,12 @@
 // every launch pays its tiles' prologues and epilogues.  Here a block takes 64 rows through
 //   forward   A_l = elu(W_l A_{l-1} + b_l)                       l = 0 .. L-1  (A_{-1} = IN)
 //   VJP       D_{L-1} = (nnT[L] X) * elu'(A_{L-1}),  D_{l-1} = (nnT[l] D_l) * elu'(A_{l-1})
-//   output    GX = [D_0 | A_{L-1}] . [nnT[0] | nn[L]]^T + b_L
+//   output    GX = [A_{L-1} | D_0] . [nn[L] | nnT[0]]^T + b_L
 // with the current 512-wide operand in a 128 KB LDS image (64 rows x 16 chunks, chunk-major so each
 // 32-deep chunk is a 64-row slab laid out like a k_gemm_x3h ring slot) and the x part of IN in a
-// 32 KB image: 160 KB, one block (8 waves, 2 per SIMD) per CU.  Only A_0 .. A_{L-1} go to HBM (the
-// VJP's elu' operands and the second half of GX's K), and GX; nothing else leaves the CU.
+// 32 KB image: 160 KB, one block (8 waves, 2 per SIMD) per CU.  GX's A_{L-1} half is formed at the
+// end of the forward, while A_{L-1} is the LDS image, and its fp32 partial sums wait in the rows'
+// GX region; only A_0 .. A_{L-2} (the VJP's elu' operands), those partial sums and GX go to HBM.
 //
 // Wave w owns units 64 w .. 64 w + 63 of every 512-wide product: its weight rows are private, so the
 // MFMA A operands come straight from global (L2-resident: 1 MB per layer shared by every block) into
@@ -355,23 +356,39 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     if (l + 1 < NL)
       pre_fwd(l + 1);
     else
-      pre_vjp(NL);
+      pre_gx(0);
     pn_barrier();  // every wave's reads of the layer input are done
-    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], L.A[l], xh, xl);
+    // A_{L-1} stays in LDS only: GX's A_{L-1} half is formed below and elu'(A_{L-1}) read from the image
+    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], l + 1 < NL ? L.A[l] : -1, xh, xl);
     pn_barrier();
+  }
+  // GX's A_{L-1} half (chunks 0 .. 15 of K) from the image; wave wv < nopt takes unit tile wv of all
+  // 64 rows.  Its fp32 partial sums go to this lane's own words of the rows' GX region (lane (il, ql)
+  // of path tile b: units 16 wv + 4 ql .. + 3 of row 16 b + il) and come back to the same lane for
+  // the D_0 half, so the accumulation order is the layer-wise GEMM's [A_{L-1} | D_0]
+  const int vpart = il * ldb + 16 * ql;  // + scalar 4 GX + 64 wv
+  {
+    pn_f4 ag[1][4];
+    pn_zero(ag);
+    if (wv < nopt) pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, 0, PN_HC, 0, il, ql, act);
+    pre_vjp(NL);
+    if (wv < nopt)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) pn_st<NTS>(rown(b), vpart, 4 * L.GX + 64 * wv, __builtin_bit_cast(u32x4_t, ag[0][b]));
   }
   // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
   // granules, so no barrier before the stores)
   {
     pn_zero(acc);
     pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[NL], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk, 0, il, ql, xsl);
-    // the forward's HBM stores of A_0 .. A_{L-1} complete (read back below: A_{l-1} by the lane that
-    // stored it, A_{L-1} by other waves for GX)
+    // the forward's HBM stores of A_0 .. A_{L-2} and the GX partial sums complete (each read back
+    // below by the lane that stored it)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (NL > 1)
       pre_vjp(NL - 1);
     else
-      pre_gx(0);
+      pre_gx(PN_HC);
+    pn_barrier();  // every wave's GX partial (all of the image) is read before the epilogue overwrites it
     epilogue(PN_DELU_LDS, pd.nnTW[NL], nullptr, -1, xh, xl);
     pn_barrier();
   }
@@ -390,36 +407,28 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     if (l > 1)
       pre_vjp(l - 1);
     else
-      pre_gx(0);
+      pre_gx(PN_HC);
     pn_barrier();
     epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, xh, xl);
     pn_barrier();
   }
-  // GX = [D_0 | A_{L-1}] . gxno^T + b_L (K = 1,024: D_0 from act, then A_{L-1} reloaded into act).
-  // Wave wv < nopt takes unit tile wv for all 64 rows, so each weight fragment is read once per
-  // block; the two tiles of a granule pair then meet in the X image (free since D_{L-1}) as fp32.
+  // GX = [A_{L-1} | D_0] . gxno^T + b_L (K = 1,024): the A_{L-1} half's partial sums back from the
+  // rows, then the D_0 half from act.  Wave wv < nopt takes unit tile wv for all 64 rows, so each
+  // weight fragment is read once per block; the two tiles of a granule pair then meet in the X image
+  // (free since D_{L-1}) as fp32.
   {
     // the lane's (il, ql) again from the hardware lane count: keeping them live across the whole
     // chain cost the register allocator a spill at the 224-register cap
     int lid;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
     const int il = lid & 15, ql = lid >> 4;
-    pn_f4 ag[1][4];
-    pn_zero(ag);
     const bool live = wv < nopt;
-    if (live) pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, 0, PN_HC, 0, il, ql, act);
-    pre_gx(PN_HC);
-    {
-      u32x4_t v[PN_HC];
-#pragma unroll
-      for (int c = 0; c < PN_HC; ++c) v[c] = pn_ld<NTS>(rr, vrow, 4 * (L.A[NL - 1] + 32 * c));
-      pn_barrier();
-#pragma unroll
-      for (int c = 0; c < PN_HC; ++c) *gdst(act(c)) = v[c];
-    }
-    pn_barrier();
     float* gx = reinterpret_cast<float*>(lds.xs);  // row m: 128 fp32
     if (live) {
+      pn_f4 ag[1][4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        ag[0][b] = __builtin_bit_cast(pn_f4, pn_ld<NTS>(rown(b), il * ldb + 16 * ql, 4 * L.GX + 64 * wv));
       pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, PN_HC, PN_HC, 0, il, ql, act);
       const float* bias = pd.nnbP[NL] + 16 * wv + 4 * ql;
 #pragma unroll

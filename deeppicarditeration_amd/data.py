@@ -213,19 +213,29 @@ class OnlineDataGenerator:
         (tx, y) from two launches — dpi_sample_points_baseline (the sampling inside the baseline
         launch), then dpi_label_moments_finalize (the label reduce inside the path launch);
         last_moments as _generate.  on_moments_*: called around the second (bench timing)."""
-        n, F, M = n_batch, 1 + self.equation.nx, self.n_estimate_integral
-        tx = torch.empty(n, F, dtype=torch.float32, device=self._device)
-        ws = self._workspace(n, M)
-        self._configure_problem()
-        _lib.check(self.lib.dpi_sample_points_baseline(self.problem, self.net.handle, n, self.seed, self.epoch,
-                                                       point_base, self.eps, self.t_factors, _ptr(tx), _ptr(ws),
-                                                       ws.numel(), _stream(self._device)), "dpi_sample_points_baseline")
+        M = self.n_estimate_integral
+        ws = self._workspace(n_batch, M)
+        tx = self.sample_points_baseline(n_batch, point_base, ws)
         if on_moments_begin:
             on_moments_begin()
         y, self.last_moments = self.label_moments_finalize(tx, point_base, M, _lib.DPI_BOTH, ws, bound)
         if on_moments_end:
             on_moments_end()
         return tx, y
+
+    def sample_points_baseline(self, n_batch, point_base, ws):
+        """Points at counters [point_base, point_base + n) sampled inside the per-point baseline
+        launch (dpi_sample_points_baseline) into ws (uint8, >= workspace_bytes): tx (n, 1+nx), bitwise
+        sample_t_and_x's, and the baseline point_baseline would leave in ws."""
+        n, F = n_batch, 1 + self.equation.nx
+        if ws.numel() < self.workspace_bytes(n, max(self.n_estimate_terminal, self.n_estimate_integral)):
+            raise ValueError("workspace too small")
+        tx = torch.empty(n, F, dtype=torch.float32, device=self._device)
+        self._configure_problem()
+        _lib.check(self.lib.dpi_sample_points_baseline(self.problem, self.net.handle, n, self.seed, self.epoch,
+                                                       point_base, self.eps, self.t_factors, _ptr(tx), _ptr(ws),
+                                                       ws.numel(), _stream(self._device)), "dpi_sample_points_baseline")
+        return tx
 
     def sample_with_gradients_and_hessians(self, n_batch):
         """data.py:225-237: (tx, clip(u_ux_uxx)) with u_ux_uxx (n, 1 + nx + nx^2)."""

@@ -137,8 +137,12 @@ class ShardedLabeler:
         with torch.cuda.stream(self._side):
             if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
                 self._side.wait_event(self._prep_free[k])
-            tx, pb = gen.sample_t_and_x(n)
-            gen.point_baseline(tx, ws=ws)
+            if hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
+                pb = gen._take_points(n)
+                tx = gen.sample_points_baseline(n, pb, ws)
+            else:
+                tx, pb = gen.sample_t_and_x(n)
+                gen.point_baseline(tx, ws=ws)
             m0, m1 = self.shard(M)
             gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
             ready = torch.cuda.Event()

@@ -17,7 +17,7 @@ NX = 100
 def _make(kind, M, K, t_uniform=True, seed=7):
     torch.manual_seed(0)
     hess = None
-    if kind == "cha":
+    if kind in ("cha", "zero"):
         eq, widths = dpi.Cha(NX, 1.0, 5.0, 1.0), [128] * 4
     elif kind == "ou":
         eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
@@ -27,8 +27,6 @@ def _make(kind, M, K, t_uniform=True, seed=7):
         eq, widths = dpi.GBMEquationComplexExact(NX, 1.0, 1.0), [64] * 3
         hess = {"method": "SDGD", "kwargs": {"v": 100}}
     net = dpi.construct_mlp(1 + NX, 1, widths, ["ELU"] * len(widths), None) if kind != "zero" else dpi.ZeroSolution(1)
-    if kind == "zero":
-        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
     return dpi.OnlineDataGenerator(eq, net, 10, 3, device="cuda:0", t_always_uniform=t_uniform, n_estimate_terminal=M,
                                    n_estimate_integral=M, n_euler_steps=K, seed=seed, hessian_approximation=hess)
 
