@@ -1014,8 +1014,9 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   // the VJP chain as one launch with the activations in LDS (dpi_pisnet.h), where the shape fits
   if (vjp && R > 0 && pis_fused_on() && pis_fused_fits(pd, L)) {
     const dim3 grid((R + PN_BM - 1) / PN_BM), block(PN_THREADS);
+    // DPI_PIS_NT: 2 (default) non-temporal row loads, plain stores; 1 both non-temporal; 0 neither
     const char* e = std::getenv("DPI_PIS_NT");
-    const bool nt = !e || std::atoi(e) != 0;
+    const int ntm = e ? (std::atoi(e) == 1 ? 3 : std::atoi(e) == 0 ? 0 : 1) : 1;
     auto launch = [&](auto ntc, auto nlc) {
       hipLaunchKernelGGL((k_pis_net<decltype(ntc)::value, decltype(nlc)::value>), grid, block, 0, st, pd, rows, L, R);
     };
@@ -1027,10 +1028,12 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
         default: launch(ntc, std::integral_constant<int, 4>{}); break;
       }
     };
-    if (nt)
-      by_depth(std::true_type{});
+    if (ntm == 1)
+      by_depth(std::integral_constant<int, 1>{});
+    else if (ntm == 3)
+      by_depth(std::integral_constant<int, 3>{});
     else
-      by_depth(std::false_type{});
+      by_depth(std::integral_constant<int, 0>{});
     return L;
   }
   int Kp = L.INP;

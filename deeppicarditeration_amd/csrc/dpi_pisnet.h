@@ -189,21 +189,24 @@ enum { PN_ELU = 0, PN_DELU_LDS = 1, PN_DELU_HBM = 2 };
 // first row and sized to its valid rows: rows past R read as zeros and their stores are dropped, so
 // the partial last tile needs no clamped addresses, and every access is one 32-bit lane offset
 // (holding the whole row offset: the range check ignores the scalar offset) plus a wave-uniform
-// scalar offset for the columns (no 64-bit per-lane pointers held across the layers).  NTS: the
-// non-temporal hint (cache policy nt), so the row streams through L2 do not evict the chain's
-// weights (7 MB, shared by every block of the XCD).
-template <bool NTS>
+// scalar offset for the columns (no 64-bit per-lane pointers held across the layers).  NTM: the
+// non-temporal hint (cache policy nt) on the row loads (bit 0), so the row streams through L2 do
+// not evict the chain's weights (7 MB, shared by every block of the XCD), and on the row stores
+// (bit 1).  Stores without it: a lane's two 16-B stores of a 32-B granule pair merge in L2 before
+// write-back; with it they leave as partial-line writes (k_pis_net's HBM writes per HJB label call
+// 2.69 GB with, 1.84 GB without, against 1.88 GB of rows written, r04i).
+template <int NTM>
 __device__ __forceinline__ u32x4_t pn_ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
-  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, NTS ? 2 : 0));
+  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, (NTM & 1) ? 2 : 0));
 }
-template <bool NTS>
+template <int NTM>
 __device__ __forceinline__ void pn_st(__amdgpu_buffer_rsrc_t r, int vo, int so, u32x4_t v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, vo,
-                                         so, NTS ? 2 : 0);
+                                         so, (NTM & 2) ? 2 : 0);
 }
 
-// R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.  NTS: the non-temporal hint on
-// the row traffic (DPI_PIS_NT, default on).  At most 232 registers per wave (VGPRs + AGPRs; the
+// R rows from rows (stride L.stride); grid = ceil(R / 64) blocks.  NTM: the non-temporal hints
+// (DPI_PIS_NT: 2 = loads only, the default; 1 = loads and stores; 0 = none).  At most 232 registers per wave (VGPRs + AGPRs; the
 // 160 KB of LDS leave none for another block): a one-wave k_pis_rollout_shared block of the next
 // batch (<= 48 VGPRs, no LDS) fits on every SIMD beside the two k_pis_net waves (2 x 232 + 48 =
 // 512).  (On gfx950 amdgpu_num_vgpr(N) caps the unified VGPR + AGPR file at 2 N: 116 -> 232; at 224
@@ -211,7 +214,7 @@ __device__ __forceinline__ void pn_st(__amdgpu_buffer_rsrc_t r, int vo, int so, 
 #ifndef DPI_PN_VGPR_HALF
 #define DPI_PN_VGPR_HALF 116  // 232 registers
 #endif
-template <bool NTS, int NL>
+template <int NTM, int NL>
 __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_PN_VGPR_HALF))) void k_pis_net(NetPisDev pd,
                                                                                                  float* __restrict__ rows,
                                                                                                  PisRows L, int R) {
@@ -321,8 +324,8 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
         u32x4_t eh, el;
         pn_split8(v, eh, el);
         if (save_reg >= 0) {  // rows past R: dropped by the buffer's range check
-          pn_st<NTS>(rown(b), vown, sown(save_reg, c), eh);
-          pn_st<NTS>(rown(b), vown, sown(save_reg, c) + 16, el);
+          pn_st<NTM>(rown(b), vown, sown(save_reg, c), eh);
+          pn_st<NTM>(rown(b), vown, sown(save_reg, c) + 16, el);
         }
         *lds_at(b, c, 0) = eh;
         *lds_at(b, c, 1) = el;
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     u32x4_t v[2 + PN_XC];
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
-      if (c < 2 + nxk) v[c] = pn_ld<NTS>(rr, vrow, 4 * (L.IN + 32 * c));
+      if (c < 2 + nxk) v[c] = pn_ld<NTM>(rr, vrow, 4 * (L.IN + 32 * c));
 #pragma unroll
     for (int c = 0; c < 2 + PN_XC; ++c)
       if (c < 2 + nxk) *gdst(c < 2 ? act(c) : xsl(c - 2)) = v[c];
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     pre_vjp(NL);
     if (wv < nopt)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) pn_st<NTS>(rown(b), vpart, 4 * L.GX + 64 * wv, __builtin_bit_cast(u32x4_t, ag[0][b]));
+      for (int b = 0; b < 4; ++b) pn_st<NTM>(rown(b), vpart, 4 * L.GX + 64 * wv, __builtin_bit_cast(u32x4_t, ag[0][b]));
   }
   // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
   // granules, so no barrier before the stores)
@@ -401,8 +404,8 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        xh[b][c] = pn_ld<NTS>(rown(b), vown, sown(L.A[l - 1], c));
-        xl[b][c] = pn_ld<NTS>(rown(b), vown, sown(L.A[l - 1], c) + 16);
+        xh[b][c] = pn_ld<NTM>(rown(b), vown, sown(L.A[l - 1], c));
+        xl[b][c] = pn_ld<NTM>(rown(b), vown, sown(L.A[l - 1], c) + 16);
       }
     if (l > 1)
       pre_vjp(l - 1);
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
       pn_f4 ag[1][4];
 #pragma unroll
       for (int b = 0; b < 4; ++b)
-        ag[0][b] = __builtin_bit_cast(pn_f4, pn_ld<NTS>(rown(b), il * ldb + 16 * ql, 4 * L.GX + 64 * wv));
+        ag[0][b] = __builtin_bit_cast(pn_f4, pn_ld<NTM>(rown(b), il * ldb + 16 * ql, 4 * L.GX + 64 * wv));
       pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, PN_HC, PN_HC, 0, il, ql, act);
       const float* bias = pd.nnbP[NL] + 16 * wv + 4 * ql;
 #pragma unroll
