@@ -98,6 +98,14 @@ __device__ __forceinline__ void x3_put4(float* row, int reg, int j, const float 
   *reinterpret_cast<uint2*>(g + 4) = make_uint2(lw[0], lw[1]);
 }
 
+// v[0..3] of dims d0 .. d0 + 3 as one 16-B store (dims >= nx as 0): a row's noise-sum region is
+// written in whole granules, not four 4-B pieces per dim-block (lane = row, so a wave's store
+// instruction touches 64 rows; fewer, larger pieces per line reach HBM as fewer partial writes)
+__device__ __forceinline__ void pis_put4(float* dst, const float (&v)[4], int d0, int nx) {
+  *reinterpret_cast<float4*>(dst) = make_float4(v[0], d0 + 1 < nx ? v[1] : 0.f, d0 + 2 < nx ? v[2] : 0.f,
+                                                d0 + 3 < nx ? v[3] : 0.f);
+}
+
 // The rollout of one (point, 64-path block) path set and ONE of its two paths, by one wave (lane =
 // path, no LDS): wave 2 g' + 0 rolls out the terminal path t -> T (S_T, g(X_T) -> a_p), wave
 // 2 g' + 1 the integral path t -> s (S_s, X_s -> the network input rows, s and its scalars).  The
@@ -148,11 +156,12 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
         const int d = 4 * j + q;
         xv[q] = d < nx ? fmaf(cT, sv[q], txr[1 + d]) : 0.f;
         if (d < nx) {
-          row[L.ST + d] = sv[q];
           if (TERM) Eq<KIND>::gstat(e, d, xv[q], gst);
           if (!X3 && stage == PIS_TD_TERM) row[L.IN + PIS_IN_OFF + d] = xv[q];  // network input X_{t_next}
         }
       }
+      // one 16-B store per dim-block (the region holds round_up(nx, 4) floats; its padding gets 0)
+      pis_put4(row + L.ST + 4 * j, sv, 4 * j, nx);
       if (X3 && stage == PIS_TD_TERM) x3_put4(row, L.IN + 64, j, xv);
     }
     if (stage == PIS_TD_TERM) {  // the network at (t_next, X_{t_next}): time input and zero padding
@@ -191,11 +200,9 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
     for (int q = 0; q < 4; ++q) {
       const int d = 4 * j + q;
       xv[q] = d < nx ? fmaf(cI, sv[q], txr[1 + d]) : 0.f;  // X_s
-      if (d < nx) {
-        row[L.SS + d] = sv[q];
-        if (!X3) row[L.IN + PIS_IN_OFF + d] = xv[q];
-      }
+      if (d < nx && !X3) row[L.IN + PIS_IN_OFF + d] = xv[q];
     }
+    pis_put4(row + L.SS + 4 * j, sv, 4 * j, nx);
     if (X3) x3_put4(row, L.IN + 64, j, xv);
   }
   if (X3) {  // the zero padding of the x part (dims nx .. INP - 64) of IN; the time input
