@@ -9,9 +9,9 @@
 //   output    GX = [A_{L-1} | D_0] . [nn[L] | nnT[0]]^T + b_L
 // with the current 512-wide operand in a 128 KB LDS image (64 rows x 16 chunks, chunk-major so each
 // 32-deep chunk is a 64-row slab laid out like a k_gemm_x3h ring slot) and the x part of IN in a
-// 32 KB image: 160 KB, one block (8 waves, 2 per SIMD) per CU.  GX's A_{L-1} half is formed at the
-// end of the forward, while A_{L-1} is the LDS image, and its fp32 partial sums wait in the rows'
-// GX region; only A_0 .. A_{L-2} (the VJP's elu' operands), those partial sums and GX go to HBM.
+// 32 KB image: 160 KB, one block (8 waves, 2 per SIMD) per CU.  GX's A_{L-1} half is formed while
+// A_{L-1} is the LDS image and its fp32 partial sums wait in the X image; only A_0 .. A_{L-2} (the
+// VJP's elu' operands) and GX go to HBM.
 //
 // Wave w owns units 64 w .. 64 w + 63 of every 512-wide product: its weight rows are private, so the
 // MFMA A operands come straight from global (L2-resident: 1 MB per layer shared by every block) into
@@ -359,39 +359,38 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     if (l + 1 < NL)
       pre_fwd(l + 1);
     else
-      pre_gx(0);
+      pre_vjp(NL);
     pn_barrier();  // every wave's reads of the layer input are done
     // A_{L-1} stays in LDS only: GX's A_{L-1} half is formed below and elu'(A_{L-1}) read from the image
     epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], l + 1 < NL ? L.A[l] : -1, xh, xl);
     pn_barrier();
   }
-  // GX's A_{L-1} half (chunks 0 .. 15 of K) from the image; wave wv < nopt takes unit tile wv of all
-  // 64 rows.  Its fp32 partial sums go to this lane's own words of the rows' GX region (lane (il, ql)
-  // of path tile b: units 16 wv + 4 ql .. + 3 of row 16 b + il) and come back to the same lane for
-  // the D_0 half, so the accumulation order is the layer-wise GEMM's [A_{L-1} | D_0]
-  const int vpart = il * ldb + 16 * ql;  // + scalar 4 GX + 64 wv
-  {
-    pn_f4 ag[1][4];
-    pn_zero(ag);
-    if (wv < nopt) pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, 0, PN_HC, 0, il, ql, act);
-    pre_vjp(NL);
-    if (wv < nopt)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) pn_st<NTM>(rown(b), vpart, 4 * L.GX + 64 * wv, __builtin_bit_cast(u32x4_t, ag[0][b]));
-  }
   // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
-  // granules, so no barrier before the stores)
+  // granules).  Between its product and its epilogue, while act still holds A_{L-1}, GX's A_{L-1}
+  // half (chunks 0 .. 15 of K): wave wv < nopt takes unit tile wv of all 64 rows, and its fp32
+  // partial sums wait in the X image (free once every wave's product has read X) at the words the
+  // same lane later writes GX to, so the accumulation order is the layer-wise GEMM's [A_{L-1} | D_0]
+  // and nothing leaves the CU.
+  float* const gxs = reinterpret_cast<float*>(lds.xs);  // row m: 128 fp32
   {
     pn_zero(acc);
     pn_gemm<4, 4>(acc, w, wsrc(pd.nnTF[NL], PN_H, 32 * nxk), vo, 4 * wv, nxk, 0, nxk, 0, il, ql, xsl);
-    // the forward's HBM stores of A_0 .. A_{L-2} and the GX partial sums complete (each read back
-    // below by the lane that stored it)
+    pre_gx(0);
+    pn_f4 ag[1][4];
+    pn_zero(ag);
+    if (wv < nopt) pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, 0, PN_HC, 0, il, ql, act);
+    // the forward's HBM stores of A_0 .. A_{L-2} complete (each read back below by the lane that
+    // stored it)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (NL > 1)
       pre_vjp(NL - 1);
     else
       pre_gx(PN_HC);
-    pn_barrier();  // every wave's GX partial (all of the image) is read before the epilogue overwrites it
+    pn_barrier();  // every wave is done with X and with all of A_{L-1}
+    if (wv < nopt)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        *reinterpret_cast<pn_f4*>(gxs + (16 * b + il) * 128 + 16 * wv + 4 * ql) = ag[0][b];
     epilogue(PN_DELU_LDS, pd.nnTW[NL], nullptr, -1, xh, xl);
     pn_barrier();
   }
@@ -416,7 +415,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     pn_barrier();
   }
   // GX = [A_{L-1} | D_0] . gxno^T + b_L (K = 1,024): the A_{L-1} half's partial sums back from the
-  // rows, then the D_0 half from act.  Wave wv < nopt takes unit tile wv for all 64 rows, so each
+  // X image, then the D_0 half from act.  Wave wv < nopt takes unit tile wv for all 64 rows, so each
   // weight fragment is read once per block; the two tiles of a granule pair then meet in the X image
   // (free since D_{L-1}) as fp32.
   {
@@ -426,12 +425,11 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
     const int il = lid & 15, ql = lid >> 4;
     const bool live = wv < nopt;
-    float* gx = reinterpret_cast<float*>(lds.xs);  // row m: 128 fp32
+    float* gx = gxs;
     if (live) {
       pn_f4 ag[1][4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        ag[0][b] = __builtin_bit_cast(pn_f4, pn_ld<NTM>(rown(b), il * ldb + 16 * ql, 4 * L.GX + 64 * wv));
+      for (int b = 0; b < 4; ++b) ag[0][b] = *reinterpret_cast<const pn_f4*>(gx + (16 * b + il) * 128 + 16 * wv + 4 * ql);
       pn_gemm<1, 4>(ag, w, rg, vo, wv, KG / 32, PN_HC, PN_HC, 0, il, ql, act);
       const float* bias = pd.nnbP[NL] + 16 * wv + 4 * ql;
 #pragma unroll
