@@ -51,12 +51,14 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 #define DPI_NOISE_UNROLL_FO 4
 #endif
 #ifndef DPI_NOISE_UNROLL_GBM
-// the same for GBM's one-wave-per-SIMD k_paths: 4 (r03aj same-box A/B, 3 pairs: 0.820-0.824 ->
-// 0.811-0.814 ms/step, k_paths 783 -> 773 us; 376 VGPRs either way)
-#define DPI_NOISE_UNROLL_GBM 4
+// the same for GBM's one-wave-per-SIMD k_paths (the sweep sets its register count, so the rollout
+// may hold more chains): 2 -> 4 r03aj (k_paths 783 -> 773 us), 4 -> 8 r04o (same-box A/B, 2 pairs:
+// 742 -> 738-740 us; 376 VGPRs either way)
+#define DPI_NOISE_UNROLL_GBM 8
 #endif
 #ifndef DPI_NOISE_UNROLL_HESS
-#define DPI_NOISE_UNROLL_HESS 1  // the Hessian-label k_paths
+// the Hessian-label k_paths: 1 -> 4 r04o (same-box A/B, 2 pairs: 1.747 -> 1.719 ms/step)
+#define DPI_NOISE_UNROLL_HESS 4
 #endif
 constexpr int NXP_MAX = 128;       // max padded state dimension
 constexpr int HMAX = 128;
@@ -605,6 +607,23 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   }
 }
 
+// Phase stamps of the GBM network launch (measurement variant only, tools/gbm_stamps.py): lanes 0-1
+// of each wave write s_memtime at fixed points into a device array (vector stores; lane-indexed).
+#ifdef DPI_GBM_STAMPS
+constexpr int DPI_STAMP_BLOCKS = 1024, DPI_STAMP_EV = 8;
+__device__ unsigned long long dpi_stamps[DPI_STAMP_BLOCKS * 4 * DPI_STAMP_EV * 2];
+#define DPI_STAMP(on, ev)                                                                                   \
+  do {                                                                                                      \
+    if ((on) && (threadIdx.x & 63) < 2 && blockIdx.x < DPI_STAMP_BLOCKS)                                    \
+      dpi_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * DPI_STAMP_EV + (ev)) * 2 + (threadIdx.x & 1)] =    \
+          __builtin_amdgcn_s_memtime();                                                                     \
+  } while (0)
+#else
+#define DPI_STAMP(on, ev) \
+  do {                    \
+  } while (0)
+#endif
+
 // LDS of the fully-nonlinear (GBM) path kernel: every weight matrix stays resident for the
 // 100-direction tangent sweep.  H <= 64, L <= 4.
 template <int H>
@@ -627,7 +646,6 @@ struct LdsGbm {
   // SDGD: each path's distinct sampled directions in increasing order (mlp_hdiag_split's sweep)
   static constexpr int DLCAP = 96;
   unsigned char dl[P * DLCAP];
-  unsigned char nd[P];
 };
 
 __device__ __forceinline__ float d2elu_from_a(float a) { return a > 0.f ? 0.f : a + 1.0f; }
@@ -784,6 +802,10 @@ template <int H, int L>
 __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
                                                 float& s1_out, float& s2_out) {
   static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
+#ifdef DPI_ABL_NOHDIAG  // measurement variant (tools/build_variant.py): no Hessian diagonal at all
+  s1_out = s2_out = 0.f;
+  return;
+#endif
   constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
   constexpr int WXS = LdsGbm<H>::WXS;
   constexpr float SA = 16.0f, SB = 64.0f;  // operand prescales: activations, tangents
@@ -972,26 +994,48 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
   // directions take the full sweep.
   int ndp = e.nx, kmax = e.nx;
   bool lists = false;
+#ifdef DPI_ABL_NOSWEEP  // measurement variant (tools/build_variant.py): no direction sweep
+  s1_out = s2_out = 0.f;
+  return;
+#endif
+#ifdef DPI_ABL_NOLISTS  // measurement variant: the full 100-direction sweep
+  if (false) {
+#else
   if (e.sdgd_v > 0) {
+#endif
     constexpr int DLCAP = LdsGbm<H>::DLCAP;
-    if (qq == 0) {
-      int k = 0;
-      for (int dd = 0; dd < e.nx; ++dd)
-        if (sh.cnt[dd * P + pp]) {
-          if (k < DLCAP) sh.dl[pp * DLCAP + k] = (unsigned char)dd;
-          ++k;
-        }
-      sh.nd[pp] = (unsigned char)min(k, 255);
+    // the path's four lanes build its list together: lane qq scans dims [qq dq, (qq + 1) dq) (all
+    // its histogram bytes read at once), places its sampled dims after the lower quarters' counts
+    // (a prefix over the path's lanes jj + 16 q), so the list is in increasing order
+    constexpr int QD = NXP_MAX / 4;
+    const int dq = (e.nx + 3) >> 2, d0 = qq * dq;
+    uint32_t mq = 0;
+#pragma unroll
+    for (int i = 0; i < QD; ++i)
+      if (i < dq && d0 + i < e.nx && sh.cnt[(d0 + i) * P + pp]) mq |= 1u << i;
+    const int cq = __popc(mq);
+    int base = 0;
+    ndp = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int v = __shfl(cq, jj + 16 * q, 64);
+      base += q < qq ? v : 0;
+      ndp += v;
     }
-    // the list of path pp is written by its lane qq = 0 and read by the path's four lanes: LDS
-    // operations of one wave complete in order; the asm keeps the compiler from hoisting the reads
+    for (int k = base; mq; ++k) {
+      const int b = __builtin_ctz(mq);
+      mq &= mq - 1;
+      if (k < DLCAP) sh.dl[pp * DLCAP + k] = (unsigned char)(d0 + b);
+    }
+    // the list of path pp is written by its four lanes and read by them: LDS operations of one wave
+    // complete in order; the asm keeps the compiler from hoisting the reads
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ndp = sh.nd[pp];
     kmax = ndp;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
     lists = kmax <= DLCAP;
   }
+  DPI_STAMP(true, 3);
   if (lists) {
     constexpr int DLCAP = LdsGbm<H>::DLCAP;
     auto dir = [&](int k) { return (int)sh.dl[pp * DLCAP + min(k, ndp - 1)]; };
@@ -1013,6 +1057,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     }
     if (d < e.nx) direction(d, za, zb, d, true);
   }
+  DPI_STAMP(true, 4);
   s1_out = s1;
   s2_out = s2;
 }
@@ -1682,8 +1727,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
-  // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM); the Hessian-label kernel's register
-  // allocation measured 4 % slower with 2
+  // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM; round 4: GBM 8, Hessian labels 4)
   constexpr int NOISE_UNROLL = HESS ? DPI_NOISE_UNROLL_HESS : GBM ? DPI_NOISE_UNROLL_GBM : DPI_NOISE_UNROLL_FO;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
@@ -1706,6 +1750,8 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   }
   const float g_x = a.gx[i], f_b = a.fb[i];
   const float Kf = (float)a.K;
+  constexpr bool STAMP = GBM && !ZERO && !HESS && !TD;
+  DPI_STAMP(STAMP, 0);
 
   for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
   const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
@@ -1995,9 +2041,12 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   } else if (!tlast) {
     terminal_rollout();
     integral_rollout();
+    DPI_STAMP(STAMP, 1);
     ap = terminal_finish();
+    DPI_STAMP(STAMP, 2);
     integrand();
     __syncthreads();
+    DPI_STAMP(STAMP, 5);
   } else {
     integral_rollout();
     __syncthreads();
@@ -2071,6 +2120,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   } else {
     if (a.tickets) fused_reduce(a, i, F, out);
   }
+  DPI_STAMP(STAMP, 6);
 }
 
 }  // namespace dpi

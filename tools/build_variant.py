@@ -1,5 +1,6 @@
-"""Build a variant libdpi_hip.so for same-box A/B runs: dpi_kernels.hip recompiled with extra
-defines, linked with the product's other objects.  usage: python tools/build_variant.py NAME -DX=Y ...
+"""Build a variant libdpi_hip.so for same-box A/B runs: dpi_kernels.hip (or the translation units
+named by --units a.hip,b.hip) recompiled with extra defines, linked with the product's other
+objects.  usage: python tools/build_variant.py NAME [--units U,..] -DX=Y ...
 -> tools/variants/libdpi_NAME.so (select it with DPI_HIP_LIB=...)."""
 import subprocess
 import sys
@@ -10,12 +11,18 @@ sys.path.insert(0, str(ROOT))
 from deeppicarditeration_amd import build as B  # noqa: E402
 
 name, defs = sys.argv[1], sys.argv[2:]
+units = ["dpi_kernels.hip"]
+if defs and defs[0] == "--units":
+    units, defs = defs[1].split(","), defs[2:]
 B.build()
 out_dir = ROOT / "tools" / "variants"
 out_dir.mkdir(exist_ok=True)
-obj = out_dir / f"dpi_kernels_{name}.o"
-subprocess.run([B.HIPCC, *B.FLAGS, *defs, "-c", "-o", str(obj), str(B.CSRC / "dpi_kernels.hip")], check=True)
-objs = [obj] + [B.OBJ / (Path(u).stem + ".o") for u in B.UNITS if u != "dpi_kernels.hip"]
+objs = []
+for u in units:
+    obj = out_dir / f"{Path(u).stem}_{name}.o"
+    subprocess.run([B.HIPCC, *B.FLAGS, *defs, "-c", "-o", str(obj), str(B.CSRC / u)], check=True)
+    objs.append(obj)
+objs += [B.OBJ / (Path(u).stem + ".o") for u in B.UNITS if u not in units]
 so = out_dir / f"libdpi_{name}.so"
 subprocess.run([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(so), *map(str, objs)], check=True)
 print(so)
