@@ -969,9 +969,37 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
     for (int l = 1; l < L; ++l) {
       half8 bh[NU], bl[NU];
+#ifdef DPI_GBM_TANGENT_2TERM
+      // measurement variant: the tangent operand as fp16 hi only, two products
+      // W_hi z_hi + W_lo z_hi per chunk; gated by the oracle (tools/build_variant.py)
+      {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = fz[l - 1][2 * u][r] * z[2 * u][r];
+            v[4 + r] = fz[l - 1][2 * u + 1][r] * z[2 * u + 1][r];
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bh[u][j] = (_Float16)v[j];
+        }
+      }
+      floatx4 o[HT];
+#pragma unroll
+      for (int T = 0; T < HT; ++T) o[T] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+#pragma unroll
+        for (int T = 0; T < HT; ++T) o[T] = mfma16(wh[l - 1][T][u], bh[u], o[T]);
+#pragma unroll
+        for (int T = 0; T < HT; ++T) o[T] = mfma16(wl[l - 1][T][u], bh[u], o[T]);
+      }
+#else
       split_b(z, fz[l - 1], bh, bl);
       floatx4 o[HT];
       wmul(l, bh, bl, o);
+#endif
 #pragma unroll
       for (int T = 0; T < HT; ++T)
 #pragma unroll
