@@ -821,8 +821,9 @@ static PisRows pis_rows_layout(const NetPisDev& pd, bool x3) {
   o += rw(pd.nx);
   L.ST = o;
   o += rw(pd.nx);
-  L.SC = o;  // s, cI, a_p, s - t, [split: network time input, smooth]
-  o += rw(8);
+  L.SC = o;  // s, cI, TD u(t_next), s - t, [split: network time input, smooth]; from PIS_GST the
+             // rollout parts' terminal GMM statistics
+  o += rw(PIS_GST + PIS_PARTS * NSG);
   L.stride = o;
   return L;
 }
@@ -1276,7 +1277,8 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
           (void)hipMemsetAsync(rq, 0, 256 + (size_t)PIS_CLAIM_SLOTS * 4, st);
           hipLaunchKernelGGL((k_pis_rollout_shared<DPI_EQ_OU, true>), dim3(4 * cu_count() * (1 + pis_prep_shared())),
                              dim3(P), 0, st, p->e, net->pis, tx, g0, a.nbp, a.m_begin, K, a.flags, a.k0, a.k1, a.c3t,
-                             a.c3s, a.c3i, a.point_base, rows, L, stage, dt, 0, 2 * gprep, rq, rq + 64, 1);
+                             a.c3s, a.c3i, a.point_base, rows, L, stage, dt, 0, 2 * PIS_PARTS * gprep, rq, rq + 64,
+                             1);
           return;
         }
       }
@@ -1284,7 +1286,7 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
       int step = gend - gbeg;
       if (prepare_only && pis_prep_per_cu() > 0) step = pis_prep_per_cu() * cu_count();
       for (int bx0 = gbeg; bx0 < gend; bx0 += step) {  // two one-wave blocks (terminal, integral) per path set
-        const dim3 grid(2 * std::min(step, gend - bx0)), block(P);
+        const dim3 grid(2 * PIS_PARTS * std::min(step, gend - bx0)), block(P);  // (path, dim part) tasks
         if (pis_rollout_unroll() == 4)
           hipLaunchKernelGGL((k_pis_rollout<DPI_EQ_OU, X3, 4>), grid, block, 0, st, p->e, net->pis, tx, g0, a.nbp,
                              a.m_begin, K, a.flags, a.k0, a.k1, a.c3t, a.c3s, a.c3i, a.point_base, rows, L, stage,

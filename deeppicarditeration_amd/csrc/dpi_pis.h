@@ -106,26 +106,35 @@ __device__ __forceinline__ void pis_put4(float* dst, const float (&v)[4], int d0
                                                 d0 + 3 < nx ? v[3] : 0.f);
 }
 
-// The rollout of one (point, 64-path block) path set and ONE of its two paths, by one wave (lane =
-// path, no LDS): wave 2 g' + 0 rolls out the terminal path t -> T (S_T, g(X_T) -> a_p), wave
-// 2 g' + 1 the integral path t -> s (S_s, X_s -> the network input rows, s and its scalars).  The
-// point's x and the GMM parameters are wave-uniform (scalar loads), each lane's noise sums run over
-// k in order (the sum of dimension d is the same sequence of adds whatever wave owns d), and no
-// wave waits for another.  Block = one wave, so a rollout wave fits on any SIMD with 64 free VGPRs —
-// beside the previous batch's k_pis_net block (2 x <= 224 VGPRs, the whole LDS) on the prepare
-// stream (dpi_label_prepare).
+// The rollout of one (point, 64-path block) path set, ONE of its two paths and ONE of PIS_PARTS
+// dim-block ranges, by one wave (lane = path, no LDS): task 2 PIS_PARTS g' + 2 q + 0 rolls out
+// dims [4 nbq q, 4 nbq (q + 1)) of the terminal path t -> T (S_T and that range's GMM statistics of
+// X_T, partial sums in SC + PIS_GST + NSG q), task 2 PIS_PARTS g' + 2 q + 1 the same dims of the
+// integral path t -> s (S_s, X_s -> the network input rows; part 0 also s and its scalars).  A
+// part is a quarter of a path's noise, so a rollout with fewer tasks than SIMDs (the prepared
+// call's head) finishes in a quarter of a one-wave rollout's latency.  The point's x and the GMM
+// parameters are wave-uniform (scalar loads), each lane's noise sums run over k in order (the sum
+// of dimension d is the same sequence of adds whatever wave owns d), and no wave waits for another;
+// k_pis_final combines the terminal statistics as (q0 + q1) + (q2 + q3).  Block = one wave, so a
+// rollout wave fits on any SIMD with 48 free registers — beside the previous batch's k_pis_net
+// block on the prepare stream (dpi_label_prepare).
+constexpr int PIS_PARTS = 4;
+constexpr int PIS_GST = 8;  // SC + PIS_GST + NSG q: terminal GMM statistics of part q
 template <int KIND, bool X3, int UNR>
 __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                  uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
                                                  uint32_t point_base, float* __restrict__ rows, const PisRows& L,
-                                                 int stage, float td_dt, int bx, bool integral) {
+                                                 int stage, float td_dt, int bx, int task) {
+  const bool integral = task & 1;
+  const int part = task >> 1;
   const int lane = threadIdx.x & 63;
   const int g = g0 + bx;  // (point, block) in point-major order
   const int i = g / nbp, blk = g - i * nbp;
   const uint32_t ig = point_base + (uint32_t)i;
   const uint32_t m = (uint32_t)(m_begin + P * blk + lane);
   const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2;
+  const int nbq = (nb + PIS_PARTS - 1) / PIS_PARTS, j0 = part * nbq, j1 = min(nb, j0 + nbq);
   const bool TERM = flags & DPI_TERMINAL, INTG = flags & DPI_INTEGRAL;
   if (integral ? stage == PIS_TD_TERM : stage == PIS_TD_INT) return;
   const float* txr = tx + (size_t)i * F;
@@ -133,12 +142,13 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
   bool td_u;
   const float tmt = pis_horizon(e, t, td_dt, td_u);
   float* row = rows + ((size_t)bx * P + lane) * L.stride;
+  const bool last = part == PIS_PARTS - 1;
   if (!integral) {  // terminal path
     const float cT = e.asq * sqrtf(tmt / Kf);
     float gst[NSG];
 #pragma unroll
     for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
-    for (int j = 0; j < nb; ++j) {
+    for (int j = j0; j < j1; ++j) {
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
       if (TERM)
 #pragma unroll UNR
@@ -166,16 +176,19 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
     }
     if (stage == PIS_TD_TERM) {  // the network at (t_next, X_{t_next}): time input and zero padding
       if (X3) {
-        for (int j = nb; j < (L.INP - 64) / 4; ++j) {
-          const float z[4] = {0.f, 0.f, 0.f, 0.f};
-          x3_put4(row, L.IN + 64, j, z);
-        }
-        row[L.SC + 4] = t + td_dt;  // k_pis_time evaluates the time networks at T - tin
-      } else {
+        if (last)
+          for (int j = nb; j < (L.INP - 64) / 4; ++j) {
+            const float z[4] = {0.f, 0.f, 0.f, 0.f};
+            x3_put4(row, L.IN + 64, j, z);
+          }
+        if (part == 0) row[L.SC + 4] = t + td_dt;  // k_pis_time evaluates the time networks at T - tin
+      } else if (part == 0) {
         for (int j = 0; j < PIS_CH; ++j) pis_embed(pn, pn.T - (t + td_dt), row + L.E, j);
       }
     }
-    row[L.SC + 2] = TERM ? Eq<KIND>::gfin(e, gst) : 0.f;  // g(X_T); k_pis_final forms a_p = g(X_T) - g(x)
+    if (TERM)  // this part's statistics of g(X_T); k_pis_final forms a_p = g(X_T) - g(x)
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) row[L.SC + PIS_GST + NSG * part + c] = gst[c];
     return;
   }
   // integral path
@@ -183,7 +196,7 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
   const float s = fmaf(U, tmt, t);
   const float smt = U * tmt;  // not s - t: that rounds to 0 in fp32 for U < ulp(t) / tmt
   const float cI = e.asq * sqrtf(smt / Kf);
-  for (int j = 0; j < nb; ++j) {
+  for (int j = j0; j < j1; ++j) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (INTG)
 #pragma unroll UNR
@@ -206,21 +219,24 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
     if (X3) x3_put4(row, L.IN + 64, j, xv);
   }
   if (X3) {  // the zero padding of the x part (dims nx .. INP - 64) of IN; the time input
-    for (int j = nb; j < (L.INP - 64) / 4; ++j) {
-      const float z[4] = {0.f, 0.f, 0.f, 0.f};
-      x3_put4(row, L.IN + 64, j, z);
-    }
-    row[L.SC + 4] = s;  // k_pis_time evaluates the time networks at T - s
-  } else {
+    if (last)
+      for (int j = nb; j < (L.INP - 64) / 4; ++j) {
+        const float z[4] = {0.f, 0.f, 0.f, 0.f};
+        x3_put4(row, L.IN + 64, j, z);
+      }
+    if (part == 0) row[L.SC + 4] = s;  // k_pis_time evaluates the time networks at T - s
+  } else if (part == 0) {
     for (int j = 0; j < PIS_CH; ++j) pis_embed(pn, pn.T - s, row + L.E, j);
   }
-  row[L.SC + 0] = s;
-  row[L.SC + 1] = cI;
-  row[L.SC + 3] = smt;
+  if (part == 0) {
+    row[L.SC + 0] = s;
+    row[L.SC + 1] = cI;
+    row[L.SC + 3] = smt;
+  }
 }
 
-// Waves 2 (bx0 + b) and 2 (bx0 + b) + 1 of the chunk: one 64-thread block per wave.  UNR
-// independent Philox chains per wave in the noise loops, <= 64 VGPRs.
+// Tasks 2 PIS_PARTS (bx0 + b) .. of the chunk: one 64-thread block per task.  UNR independent
+// Philox chains per wave in the noise loops, <= 64 VGPRs.
 template <int KIND, bool X3, int UNR = 4>
 __global__ __launch_bounds__(64, 8) void k_pis_rollout(EqDev e, NetPisDev pn, const float* __restrict__ tx, int g0,
                                                     int nbp, int m_begin, int K, int flags, uint32_t k0, uint32_t k1,
@@ -228,7 +244,8 @@ __global__ __launch_bounds__(64, 8) void k_pis_rollout(EqDev e, NetPisDev pn, co
                                                     float* __restrict__ rows, PisRows L, int stage, float td_dt,
                                                     int bx0) {
   pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
-                                  stage, td_dt, bx0 + (int)(blockIdx.x >> 1), blockIdx.x & 1);
+                                  stage, td_dt, bx0 + (int)(blockIdx.x / (2 * PIS_PARTS)),
+                                  (int)(blockIdx.x % (2 * PIS_PARTS)));
 }
 
 // The prepare stream's rollout (dpi_label_prepare), beside the previous batch's k_pis_net: a
@@ -257,14 +274,15 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
   const int lane = threadIdx.x & 63;
   int old = 0;
   if (lane == 0) old = atomicAdd(claim + slot, 1);
-  if (__shfl(old, 0, 64) >= waves) return;  // this SIMD already runs `waves` rollout waves of this launch
+  // (lane 0's values made wave-uniform scalars: the task's indices then live in SGPRs)
+  if (__builtin_amdgcn_readfirstlane(old) >= waves) return;  // this SIMD already runs `waves` rollout waves
   for (;;) {
     int t = 0;
     if (lane == 0) t = atomicAdd(queue, 1);
-    t = __shfl(t, 0, 64);
+    t = __builtin_amdgcn_readfirstlane(t);
     if (t >= ntask) break;
     pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
-                                    stage, td_dt, bx0 + (t >> 1), t & 1);
+                                    stage, td_dt, bx0 + t / (2 * PIS_PARTS), t % (2 * PIS_PARTS));
   }
 }
 
@@ -709,9 +727,25 @@ __global__ __launch_bounds__(256) void k_pis_final(EqDev e, NetPisDev pn, const 
   const float f_b = fbv[i];
   const int p = tid >> 2, q = tid & 3;
   const float* row = rows + ((size_t)blockIdx.x * P + p) * L.stride;
-  // a_p = g(X_T) - g(x) (TD: u(t_next, X) - g(x) where t_next < T); the terminal wave wrote 0 for
-  // integral-only calls
-  const float s = row[L.SC + 0], ap = TERM ? row[L.SC + 2] - gxv[i] : 0.f, smt = row[L.SC + 3];
+  // a_p = g(X_T) - g(x), g(X_T) from the rollout parts' statistics combined as (q0 + q1) + (q2 + q3)
+  // (TD: u(t_next, X) - g(x) where t_next < T, u from k_pis_tvalue)
+  float ap = 0.f;
+  if (TERM) {
+    float gv;
+    if (td_u) {
+      gv = row[L.SC + 2];
+    } else {
+      static_assert(PIS_PARTS == 4, "the fixed combine order below");
+      float st[NSG];
+      const float* gp = row + L.SC + PIS_GST;
+#pragma unroll
+      for (int c = 0; c < NSG; ++c)
+        st[c] = (gp[c] + gp[NSG + c]) + (gp[2 * NSG + c] + gp[3 * NSG + c]);
+      gv = Eq<KIND>::gfin(e, st);
+    }
+    ap = gv - gxv[i];
+  }
+  const float s = row[L.SC + 0], smt = row[L.SC + 3];
   float A, B, sm;
   pis_z_stats<X3>(e, pn, gmm, row, L, pn.T - s, q, A, B, sm);
   const float bp = INTG ? tmt * (Eq<KIND>::ffv(e, 0.f, 0.f, A, B) - f_b) : 0.f;
