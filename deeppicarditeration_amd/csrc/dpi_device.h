@@ -1756,7 +1756,11 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
   // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM; round 4: GBM 8, Hessian labels 4)
-  constexpr int NOISE_UNROLL = HESS ? DPI_NOISE_UNROLL_HESS : GBM ? DPI_NOISE_UNROLL_GBM : DPI_NOISE_UNROLL_FO;
+  // (the u = 0 GBM instance keeps 4: at 8 its own allocation grew and the noise-floor launch ran
+  // 801 K -> 1,077 K cycles, profiles/r04s_pmc / valu_gbm.json)
+  constexpr int NOISE_UNROLL = HESS ? DPI_NOISE_UNROLL_HESS
+                               : GBM ? (ZERO ? 4 : DPI_NOISE_UNROLL_GBM)
+                                     : DPI_NOISE_UNROLL_FO;
   using SH = std::conditional_t<GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
