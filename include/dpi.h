@@ -171,7 +171,9 @@ int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint3
 int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
                         int t_factors, float* tx, void* stream);
 
-/* Per-point baseline g(x), f(t, x, u, grad u) (+ network terms) into the workspace. */
+/* Per-point baseline g(x), f(t, x, u, grad u) (+ network terms) into the workspace.  For a
+ * PISGradNet net it launches nothing: each label call forms g(x) and f_b in its first path chunk
+ * (the baseline rows ride in the k_pis_net chain, g(x) in k_pis_base_final). */
 int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes,
                        void* stream);
 
