@@ -232,7 +232,7 @@ def main():
     # PISGradNet (hjb): the next batch's rollout runs on the side stream beside this batch's k_pis_net,
     # one wave per SIMD (k_pis_rollout_shared) — the default for that workload
     args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis"))) and not args.no_prepare
-    if args.prepare:
+    if args.prepare and os.environ.get("DPI_BENCH_MAIN_PRIORITY", "high") == "high":
         lo, hi = torch.cuda.Stream.priority_range()
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=hi))
     dist = None

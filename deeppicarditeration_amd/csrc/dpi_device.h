@@ -56,6 +56,9 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 // 742 -> 738-740 us; 376 VGPRs either way)
 #define DPI_NOISE_UNROLL_GBM 8
 #endif
+#ifndef DPI_GBM_WAGPR
+#define DPI_GBM_WAGPR 1
+#endif
 #ifndef DPI_NOISE_UNROLL_HESS
 // the Hessian-label k_paths: 1 -> 4 r04o (same-box A/B, 2 pairs: 1.747 -> 1.719 ms/step)
 #define DPI_NOISE_UNROLL_HESS 4
@@ -826,6 +829,17 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     for (int T = 0; T < HT; ++T)
 #pragma unroll
       for (int u = 0; u < NU; ++u) afrag(net.WU[l], 16 * T + jj, u, wh[l - 1][T][u], wl[l - 1][T][u]);
+#if DPI_GBM_WAGPR
+  // the resident weight fragments pinned to AGPRs (MFMA reads its A operand from either file), so
+  // more of the sweep's accumulators stay in VGPRs: GBM k_paths 742 -> 735-736 us, Hessian labels
+  // unchanged (same-box pairs, r04t; DPI_GBM_WAGPR=0 builds without)
+#pragma unroll
+  for (int l = 1; l < L; ++l)
+#pragma unroll
+    for (int T = 0; T < HT; ++T)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) asm volatile("" : "+a"(wh[l - 1][T][u]), "+a"(wl[l - 1][T][u]));
+#endif
   // B operand (C layout, HT tiles x 4) x scale -> split halves per 32-wide chunk
   auto split_b = [&](const float (&x)[HT][4], const float (&f)[HT][4], half8 (&bh)[NU], half8 (&bl)[NU]) {
 #pragma unroll

@@ -1,22 +1,18 @@
 #!/bin/bash
-# r04: N=2 rehearsals (gloo, one shared GPU) on the current code; VALU/MFMA PMC passes of the
-# first-order and GBM benches.  usage: tools/gpu_r04.sh <tag>
-out=gpurun_out/${1:-r04q}; mkdir -p $out; export TMPDIR=/tmp
+# r04u: GBM with AGPR-pinned weights as the product: GBM / Hessian / TD GPU tests, bench lines.
+out=gpurun_out/${1:-r04u}; mkdir -p $out; export TMPDIR=/tmp
 set -e
-R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1"
-export DPI_BENCH_BACKEND=gloo DPI_BENCH_SHARE_GPU=1
-tools/gpu_check.sh 300 $out/rehearsal_burgers_n2.log $R --master-port 29521 bench.py --gpus 2 --workload burgers --steps 10 --warmup 2
-tools/gpu_check.sh 300 $out/rehearsal_burgers_cfg3_n2.log $R --master-port 29522 bench.py --gpus 2 --workload burgers_cfg3 --steps 10 --warmup 2
-tools/gpu_check.sh 300 $out/rehearsal_hjb_n2.log $R --master-port 29523 bench.py --gpus 2 --workload hjb --steps 6 --warmup 2
-unset DPI_BENCH_BACKEND DPI_BENCH_SHARE_GPU
-grep -h '^{' $out/rehearsal_*.log | python -c "
-import sys, json
-for l in sys.stdin:
-    d = json.loads(l); p = d['config'].get('rel_l2_vs_ref', {})
-    print(d['workload_key'], d['n_gpus'], d['config'].get('mc_paths_per_gpu'), round(d['ms_per_step'], 4), p.get('bit_identical_to_single_call'), p.get('grad'))
-"
-for wl in burgers gbm gbm_hess; do
-  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-    --kernel-include-regex k_paths -d $out/pmc_valu_$wl -o pmc --output-format csv -- \
-    python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu_$wl.log 2>&1
+tools/gpu_check.sh 600 $out/gpu_tests.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "gbm or GBM or sdgd or SDGD or hess or td or TD"
+tail -1 $out/gpu_tests.log
+S='import json,sys; d=json.loads(sys.stdin.read()); print(sys.argv[1], round(d["ms_per_step"],4), "%.3e" % d["value"], round(d["roofline"]["kernel_ms"],4), d["config"]["rel_l2_vs_ref"]["grad"])'
+B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline"
+for w in gbm gbm_hess; do
+  tools/gpu_check.sh 300 $out/$w.log $B --workload $w
+  grep -h '^{' $out/$w.log | python -c "$S" $w || true
+done
+for r in a b; do
+  tools/gpu_check.sh 300 $out/hjb_hi_$r.log $B --workload hjb
+  grep -h '^{' $out/hjb_hi_$r.log | python -c "$S" hjb_hi_$r || true
+  DPI_BENCH_MAIN_PRIORITY=default tools/gpu_check.sh 300 $out/hjb_def_$r.log $B --workload hjb
+  grep -h '^{' $out/hjb_def_$r.log | python -c "$S" hjb_def_$r || true
 done
