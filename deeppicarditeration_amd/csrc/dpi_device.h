@@ -646,8 +646,9 @@ struct LdsGbm {
   float tau[P], cmul[P], bsh[P], fbp[P];
   float smt[P];                    // Hessian labels: s - t per path
   unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
-  // SDGD: each path's distinct sampled directions in increasing order (mlp_hdiag_split's sweep)
-  static constexpr int DLCAP = 96;
+  // SDGD: each path's distinct sampled directions in increasing order (mlp_hdiag_split's sweep;
+  // H >= 32 only — the u = 0 and H = 16 instances keep their LDS under 80 KB, two blocks per CU)
+  static constexpr int DLCAP = H >= 32 ? 96 : 1;
   unsigned char dl[P * DLCAP];
 };
 
