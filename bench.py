@@ -265,7 +265,9 @@ def main():
     # the per-call range guard (a stream synchronisation per label call, OnlineDataGenerator.range_check)
     # is off in the timed pipeline: the labels' finiteness is asserted after the timed region instead
     gen.range_check = False
-    labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD)
+    # PISGradNet under the prepare schedule: each prepare() samples the next batch's points ahead
+    labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD,
+                             sample_ahead=bool(wl.get("pis")) and os.environ.get("DPI_BENCH_SAMPLE_AHEAD", "1") == "1")
 
     # path-kernel timing with events on the stream the kernels run on (torch's current stream)
     ev = []

@@ -25,11 +25,18 @@ class ShardBitIdentityWarning(UserWarning):
 
 
 class ShardedLabeler:
-    def __init__(self, gen, rank=0, world=1, group=None):
+    def __init__(self, gen, rank=0, world=1, group=None, sample_ahead=False):
+        """sample_ahead (PISGradNet, prepare()): each prepare() also samples the NEXT batch's points,
+        on a stream of their own, so the next prepare's rollout does not wait for a sampling launch
+        on the side stream's critical path.  The batches get the same point ranges in the same
+        order (under the generator's seed and epoch at the prepare() that samples them); the points
+        sampled ahead of the last prepare() are skipped."""
         self.gen = gen
         self.rank = rank
         self.world = world
         self.group = group
+        self.sample_ahead = sample_ahead
+        self._ahead = None
 
     def shard(self, M):
         blk = 64
@@ -134,10 +141,19 @@ class ShardedLabeler:
         self._prep_next = (k + 1) % 3
         self._prep_busy[k] = True
         ws = self._prep_ws[k]
+        # PISGradNet only: its points need no workspace (the baseline lives in the label call)
+        pis = str(getattr(getattr(gen, "net", None), "desc", "")).startswith("pisgrad")
+        ahead, self._ahead = self._ahead, None
+        if ahead is not None and ahead[0] != n:
+            ahead = None  # another batch size: those points are skipped
         with torch.cuda.stream(self._side):
             if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
                 self._side.wait_event(self._prep_free[k])
-            if hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
+            if ahead is not None:
+                _, tx, pb, ev = ahead
+                self._side.wait_event(ev)
+                tx.record_stream(self._side)
+            elif hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
                 pb = gen._take_points(n)
                 tx = gen.sample_points_baseline(n, pb, ws)
             else:
@@ -148,6 +164,15 @@ class ShardedLabeler:
             ready = torch.cuda.Event()
             ready.record(self._side)
         tx.record_stream(cur)
+        if self.sample_ahead and pis:
+            if getattr(self, "_samp", None) is None:
+                self._samp = torch.cuda.Stream(device=gen.device)
+            with torch.cuda.stream(self._samp):
+                pb2 = gen._take_points(n)
+                tx2, _ = gen.sample_t_and_x(n, point_base=pb2)
+                ev2 = torch.cuda.Event()
+                ev2.record(self._samp)
+            self._ahead = (n, tx2, pb2, ev2)
         return tx, pb, ws, ready, k, flags
 
     def begin(self, tx=None, point_base=None, flags=None, on_moments_begin=None, on_moments_end=None,

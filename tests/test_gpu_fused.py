@@ -120,3 +120,26 @@ def test_label_calls_write_nothing_past_the_workspace(kind):
     torch.cuda.synchronize()
     assert torch.isfinite(mom).all()
     assert bool((buf[need:] == 0xA5).all())
+
+
+def test_prepare_with_points_sampled_ahead_equals_labels():
+    """ShardedLabeler(sample_ahead=True) (PISGradNet, the bench's HJB schedule): every prepared batch
+    gets the next consecutive point range, and its labels equal labels() on the same points."""
+    torch.manual_seed(0)
+    eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=NX, g0=eq.g, T=1.0)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=4, seed=5)
+    lab = ShardedLabeler(gen, sample_ahead=True)
+    got = []
+    for _ in range(3):
+        prep = lab.prepare(3)
+        got.append((prep[0], prep[1], lab.end(lab.begin(prepared=prep))))
+    torch.cuda.synchronize()
+    ref = ShardedLabeler(gen)
+    for b, (tx, pb, y) in enumerate(got):
+        assert pb == got[0][1] + 3 * b
+        tx0, _ = gen.sample_t_and_x(3, point_base=pb)
+        assert torch.equal(tx, tx0)
+        assert torch.equal(y, ref.labels(tx, pb))
