@@ -1,15 +1,15 @@
 #!/bin/bash
-# r04za: PIS points sampled one prepare() ahead on their own stream: PIS tests; HJB A/B (same box).
-out=gpurun_out/${1:-r04z}; mkdir -p $out; export TMPDIR=/tmp
+# r04: N=2 rehearsals (gloo, one shared GPU) on the current code.  usage: tools/gpu_r04.sh <tag>
+out=gpurun_out/${1:-r04q}; mkdir -p $out; export TMPDIR=/tmp
 set -e
-tools/gpu_check.sh 600 $out/gpu_tests.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "pis or hjb or ou or PIS or side or prepare or shard"
-tail -1 $out/gpu_tests.log
-grep -E "FAILED" $out/gpu_tests.log | head -20 || true
-S='import json,sys; d=json.loads(sys.stdin.read()); print(sys.argv[1], round(d["ms_per_step"],4), "%.3e" % d["value"], round(d["roofline"]["kernel_ms"],4), d["config"]["rel_l2_vs_ref"]["grad"])'
-B="python bench.py --steps 20 --warmup 3 --no-cpu-baseline"
-for r in a b; do
-  tools/gpu_check.sh 300 $out/hjb_ahead_$r.log $B --workload hjb
-  grep -h '^{' $out/hjb_ahead_$r.log | python -c "$S" hjb_ahead_$r || true
-  DPI_BENCH_SAMPLE_AHEAD=0 tools/gpu_check.sh 300 $out/hjb_noahead_$r.log $B --workload hjb
-  grep -h '^{' $out/hjb_noahead_$r.log | python -c "$S" hjb_noahead_$r || true
-done
+R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1"
+export DPI_BENCH_BACKEND=gloo DPI_BENCH_SHARE_GPU=1
+tools/gpu_check.sh 300 $out/rehearsal_burgers_cfg3_n2.log $R --master-port 29522 bench.py --gpus 2 --workload burgers_cfg3 --steps 10 --warmup 2
+tools/gpu_check.sh 300 $out/rehearsal_hjb_n2.log $R --master-port 29523 bench.py --gpus 2 --workload hjb --steps 6 --warmup 2
+unset DPI_BENCH_BACKEND DPI_BENCH_SHARE_GPU
+grep -h '^{' $out/rehearsal_*.log | python -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); p = d['config'].get('rel_l2_vs_ref', {})
+    print(d['workload_key'], d['n_gpus'], d['config'].get('mc_paths_per_gpu'), round(d['ms_per_step'], 4), p.get('bit_identical_to_single_call'), p.get('grad'))
+"
