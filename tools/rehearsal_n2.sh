@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: N=2 rehearsals (gloo, one shared GPU) on the current code.  usage: tools/gpu_r04.sh <tag>
+# N=2 rehearsals of the bench's N > 1 path (gloo, two ranks on one shared GPU).  usage: tools/rehearsal_n2.sh <tag>
 out=gpurun_out/${1:-r04q}; mkdir -p $out; export TMPDIR=/tmp
 set -e
 R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1"
