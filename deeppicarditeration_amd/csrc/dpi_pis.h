@@ -294,9 +294,16 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
 #define DPI_PIS_SHARED_CALL \
   e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L, stage, td_dt, bx0, ntask, queue, claim, waves
 // one wave per SIMD: 4 Philox chains per wave, <= 48 registers (beside two 232-register k_pis_net waves)
+#ifndef DPI_PIS_SHARED_VGPR_HALF
+#define DPI_PIS_SHARED_VGPR_HALF 24  // 48 registers
+#endif
+#ifndef DPI_PIS_SHARED_UNR
+#define DPI_PIS_SHARED_UNR 4
+#endif
 template <int KIND, bool X3>
-__global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(24))) void k_pis_rollout_shared(DPI_PIS_SHARED_ARGS) {
-  pis_rollout_shared_body<KIND, X3, 4>(DPI_PIS_SHARED_CALL);
+__global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(DPI_PIS_SHARED_VGPR_HALF))) void k_pis_rollout_shared(
+    DPI_PIS_SHARED_ARGS) {
+  pis_rollout_shared_body<KIND, X3, DPI_PIS_SHARED_UNR>(DPI_PIS_SHARED_CALL);
 }
 #undef DPI_PIS_SHARED_ARGS
 #undef DPI_PIS_SHARED_CALL
