@@ -92,6 +92,12 @@ def parse():
                                                            "baseline on a low-priority side stream, the path "
                                                            "kernels on a high-priority stream")
     ap.add_argument("--no-prepare", action="store_true", help="one stream (overrides --prepare and the hjb default)")
+    ap.add_argument("--range-check", choices=("step", "region", "off"), default="step",
+                    help="the product's range guard (data.RangeGroup) inside the timed region: 'step' (default) = "
+                         "one group per step, verified one step behind as the dataset surface does per label "
+                         "buffer; 'region' = one group over the timed steps, as picard train's LabelBuffer.fill; "
+                         "'off' = unguarded (finiteness asserted afterwards)")
+    ap.add_argument("--no-fp32-pass", action="store_true", help="skip the untimed exact-fp32 comparison pass")
     return ap.parse_args()
 
 
@@ -262,9 +268,11 @@ def main():
     hess = {"method": "SDGD", "kwargs": {"v": wl["sdgd"]}} if wl["sdgd"] else None
     gen = dpi.OnlineDataGenerator(eq, net, 80, 1, device=dev, t_always_uniform=True, n_estimate_terminal=M,
                                   n_estimate_integral=M, n_euler_steps=K_STEPS, seed=1, hessian_approximation=hess)
-    # the per-call range guard (a stream synchronisation per label call, OnlineDataGenerator.range_check)
-    # is off in the timed pipeline: the labels' finiteness is asserted after the timed region instead
-    gen.range_check = False
+    # The product's range guard (OnlineDataGenerator.range_check, on by default) runs inside the timed
+    # region: each step's label calls form a RangeGroup (their reductions flag into the group's slot of
+    # the net's host-visible status ring), verified one step behind — an event wait for work the GPU
+    # finished while it runs the next step, then a host read of the slot.
+    gen.range_check = args.range_check != "off"
     # PISGradNet under the prepare schedule: each prepare() samples the next batch's points ahead
     labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD,
                              sample_ahead=bool(wl.get("pis")) and os.environ.get("DPI_BENCH_SAMPLE_AHEAD", "1") == "1")
@@ -332,10 +340,36 @@ def main():
             ev.append((e0, e1))
         return y
 
+    # RangeGroups of the steps not yet verified ("step": one per step, verified one step behind;
+    # "region": one over a whole phase, verified after its drain)
+    groups = []
+    region = [None]
+    raw_step = step
+
+    def step():
+        if args.range_check != "step":
+            return raw_step()
+        with gen.deferred_range_check() as grp:
+            y = raw_step()
+        groups.append(grp)
+        if len(groups) > 2:  # the group before the previous one: its batches have all ended
+            groups.pop(0).verify()
+        return y
+
+    def open_region():
+        if args.range_check == "region":
+            region[0] = gen.deferred_range_check()
+
     def drain():
         y = None
         while pending:
             y = finish(pending.pop(0))
+        if region[0] is not None:
+            region[0].close()
+            groups.append(region[0])
+            region[0] = None
+        while groups:
+            groups.pop(0).verify()
         return y
 
     # Clock ramp: the GPU needs ~10 ms of load to leave its idle clocks, which a 20-step run at
@@ -344,6 +378,7 @@ def main():
     # then the W warmup steps of the contract.
     prewarm = 0
     t_pw = time.perf_counter()
+    open_region()
     while True:
         for _ in range(16):
             step()
@@ -365,9 +400,11 @@ def main():
     torch.cuda.synchronize()
     capture["armed"] = True
     t0 = time.perf_counter()
+    open_region()
     for _ in range(args.steps):
         y = step()
-    y = drain() if pipelined else y
+    y2 = drain()  # every pending batch ended and every range group verified, inside the timed region
+    y = y2 if pipelined else y
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -382,12 +419,37 @@ def main():
     if rank == 0 and world > 1:
         # the sharded labels against ONE call over all M paths of the same batch on this GPU (after
         # the timed region): bit-identical when M / (64 N) is a power of two
-        y1 = ShardedLabeler(gen, rank=0, world=1).labels(capture["tx"], capture["pb"])
+        one = ShardedLabeler(gen, rank=0, world=1)
+        y1 = (one.labels_hessians if wl.get("hess") else one.labels)(capture["tx"], capture["pb"])
         parity["bit_identical_to_single_call"] = bool(torch.equal(y1, capture["y"]))
         parity["max_abs_diff_to_single_call"] = float((y1 - capture["y"]).abs().max())
     # Noise floor of the same launch (untimed, after the timed region): the identical rollout with
     # u = 0 (ZeroSolution: same Philox streams, same K-step EM, no network), i.e. the
     # Philox4x32-10 + Box-Muller VALU issue the noise contract fixes.
+    # What the fp16-split MFMA buys: the same schedule with this net on exact-fp32 MFMA
+    # (dpi_net_set_precision, = DPI_GEMM=f32), untimed by the contract's clock, after the timed region
+    exact_fp32_ms = None
+    if not args.no_fp32_pass and os.environ.get("DPI_GEMM", "") != "f32":
+        gen.net.set_precision(L.DPI_GEMM_F32)
+        for _ in range(2):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        n32 = max(4, min(args.steps, 10))
+        tf = time.perf_counter()
+        open_region()
+        for _ in range(n32):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        exact_fp32_ms = (time.perf_counter() - tf) / n32 * 1e3
+        if dist:
+            t = torch.tensor([exact_fp32_ms], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            exact_fp32_ms = float(t[0])
+        gen.net.set_precision(-1)
     floor_ms = None
     if rank == 0 and not wl.get("pis") and not wl.get("hess") and "m_total" not in wl:
         gen0 = dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(1), 80, 1, device=dev, t_always_uniform=True,
@@ -484,6 +546,14 @@ def main():
                        "schedule": ("two-phase, next batch prepared on a side stream" if args.prepare and pipelined
                                     else "two-phase (all-gather overlapped)" if pipelined else "one labels() call"),
                        "prewarm_steps": prewarm,
+                       "range_check": args.range_check != "off",
+                       "range_check_mode": {"step": "one RangeGroup per step, verified one step behind (the dataset "
+                                                    "surface's per-buffer check)",
+                                            "region": "one RangeGroup over the timed steps (picard train's "
+                                                      "LabelBuffer.fill)",
+                                            "off": "unguarded"}[args.range_check],
+                       "value_is": ("whole-job total over all N GPUs (the bench contract); the per-GPU figure the "
+                                    "metric names is per_gpu_value"),
                        "rel_l2_vs_ref": parity},
             "roofline": {"bound": "valu" if valu else "mfma", **({k: valu[k] for k in ("achieved", "peak", "unit", "frac")}
                                                                   if valu else
@@ -498,6 +568,12 @@ def main():
         }
         if "survey_flop" in wl:
             out["roofline"]["mfma"]["survey_flop_per_path_label"] = wl["survey_flop"]
+        out["roofline"]["exact_fp32_ms"] = exact_fp32_ms
+        if exact_fp32_ms is not None:
+            out["roofline"]["exact_fp32"] = {
+                "what": "ms/step of the same schedule with the network on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, "
+                        "dpi_net_set_precision = DPI_GEMM=f32), untimed passes after the timed region",
+                "ms_per_step": exact_fp32_ms, "split_speedup": exact_fp32_ms / ms_step}
         if floor_ms is not None:
             out["roofline"]["noise_floor"] = {
                 "what": "same launch with u = 0 (ZeroSolution): Philox4x32-10 + Box-Muller + K-step EM only, the "

@@ -10,7 +10,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("DPI_HIP_LIB", _HERE / "libdpi_hip.so"))
 
 # constants mirrored from include/dpi.h (checked against the header by tests/test_capi.py)
-DPI_ABI_VERSION = 2
+DPI_ABI_VERSION = 3
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
@@ -21,6 +21,7 @@ DPI_PATH_BLOCK = 64
 DPI_PATHS_PER_CALL_MAX = 1024 * DPI_PATH_BLOCK
 DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
 DPI_STATUS_NONFINITE = 1
+DPI_STATUS_SLOTS = 64
 
 c_int, c_double, c_float, c_size_t, c_void_p, c_uint32, c_uint64 = (
     ctypes.c_int, ctypes.c_double, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64)
@@ -44,6 +45,9 @@ SIGNATURES = {
     "dpi_set_gemm_precision": (c_int, [c_int]),
     "dpi_net_set_precision": (c_int, [c_void_p, c_int]),
     "dpi_net_status": (c_int, [c_void_p, c_int, c_void_p, P(c_int)]),
+    "dpi_net_status_slot": (c_int, [c_void_p, c_int, c_int]),
+    "dpi_net_status_peek": (c_int, [c_void_p, c_int, P(c_int)]),
+    "dpi_build_id": (c_int, [ctypes.c_char_p, c_size_t]),
     "dpi_workspace_bytes": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_sample_points": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_void_p, c_void_p]),
     "dpi_sample_points_t": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int, c_void_p,
@@ -100,9 +104,32 @@ def load(path=None):
         fn.argtypes = args
     if lib.dpi_abi_version() != DPI_ABI_VERSION:
         raise DPIError(f"ABI mismatch: library {lib.dpi_abi_version()} != {DPI_ABI_VERSION}")
+    check_build_id(lib, p)
     if path is None:
         _lib = lib
     return lib
+
+
+def build_id(lib):
+    buf = ctypes.create_string_buffer(80)
+    lib.dpi_build_id(buf, 80)
+    return buf.value.decode()
+
+
+def check_build_id(lib, path):
+    """The in-tree library must have been built from the tree's sources (build.source_hash): a
+    library built from other sources would run kernels the tests and the bench do not describe.
+    Skipped for an explicit DPI_HIP_LIB (A/B variants, tools/build_variant.py) and where the
+    sources are absent."""
+    if "DPI_HIP_LIB" in os.environ or Path(path).resolve() != (_HERE / "libdpi_hip.so").resolve():
+        return
+    from . import build as B
+    if not B.CSRC.is_dir():
+        return
+    want, got = B.source_hash(), build_id(lib)
+    if got != want:
+        raise DPIError(f"{path} was built from other sources (build id {got[:12]}, tree {want[:12]}): rebuild it with "
+                       "`python -m deeppicarditeration_amd.build` (hipcc --offload-arch=gfx950)")
 
 
 def last_error(lib=None):

@@ -2,7 +2,11 @@
 
 Seven translation units (the C-ABI / PIS / reduce TU, one k_paths family per equation and one
 TD-estimator k_paths family per equation) compile in parallel to objects, then link into one
-shared library."""
+shared library together with a generated one-function unit, `dpi_build_id()`, that returns the
+SHA-256 of the sources and flags (`source_hash`).  The same hash goes into `libdpi_hip.so.buildid`
+beside the library: a build is current when that file matches the tree's hash (not by mtime), and
+`_lib.load()` refuses a library whose embedded identity differs from the tree it is loaded from."""
+import hashlib
 import os
 import subprocess
 import sys
@@ -24,11 +28,26 @@ def sources():
     return [CSRC / u for u in UNITS] + sorted(CSRC.glob("*.h")) + [REPO / "include" / "dpi.h"]
 
 
+BUILD_ID_FILE = OUT.with_name(OUT.name + ".buildid")
+
+
+def source_hash():
+    """SHA-256 (hex) of everything the library is compiled from: every csrc/*.hip and *.h, the
+    C-ABI header, the unit list and the compiler flags."""
+    h = hashlib.sha256()
+    h.update(repr((UNITS, FLAGS[:-1])).encode())  # the -I path differs between checkouts
+    files = sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.h")) + [REPO / "include" / "dpi.h"]
+    for f in files:
+        h.update(f.relative_to(REPO).as_posix().encode() + b"\0")
+        h.update(f.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
 def needs_build():
-    if not OUT.exists():
+    if not OUT.exists() or not BUILD_ID_FILE.exists():
         return True
-    t = OUT.stat().st_mtime
-    return any(p.stat().st_mtime > t for p in sources())
+    return BUILD_ID_FILE.read_text().strip() != source_hash()
 
 
 def build(force=False, verbose=True):
@@ -55,11 +74,29 @@ def build(force=False, verbose=True):
     with ThreadPoolExecutor(max_workers=max(1, len(todo))) as ex:
         list(ex.map(compile_unit, todo))
     objs = [OBJ / (Path(u).stem + ".o") for u in UNITS]
-    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
+    bid = source_hash()
+    objs.append(build_id_object(bid))
+    tmp = OUT.with_name(OUT.name + ".tmp")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)  # a new inode: a process that has the old library mapped keeps it intact
+    BUILD_ID_FILE.write_text(bid + "\n")
     return OUT
+
+
+def build_id_object(bid, out_dir=OBJ):
+    """The generated unit exporting dpi_build_id() (include/dpi.h) for hash `bid`, compiled."""
+    src = out_dir / "dpi_build_id.c"
+    obj = out_dir / "dpi_build_id.o"
+    src.write_text('#include <stddef.h>\n#include <string.h>\n'
+                   f'static const char k_id[] = "{bid}";\n'
+                   'int dpi_build_id(char* buf, size_t len) {\n'
+                   '  if (buf && len) { strncpy(buf, k_id, len - 1); buf[len - 1] = 0; }\n'
+                   '  return (int)(sizeof(k_id) - 1);\n}\n')
+    subprocess.run(["gcc", "-O2", "-fPIC", "-c", "-o", str(obj), str(src)], check=True)
+    return obj
 
 
 def kernel_resources(lib=OUT):

@@ -20,8 +20,14 @@ struct dpi_net_s {
   int n_in = 0;
   int precision = -1;     // DPI_GEMM_* for this net (dpi_net_set_precision); -1: the process-wide mode
   bool finite = true;     // every uploaded parameter finite
-  int* status = nullptr;  // device word, sticky: DPI_STATUS_* bits the label reductions set (dpi_net_status)
+  // Range-guard ring (dpi_net_status*): DPI_STATUS_SLOTS sticky words, one per 64-B line, in
+  // fine-grained pinned host memory; `status` is its device address, `status_host` the host one.
+  // The label reductions store DPI_STATUS_* bits into slot `slot`, selected at enqueue time.
+  int* status = nullptr;
+  int* status_host = nullptr;
+  int slot = 0;
 };
+constexpr int STATUS_STRIDE = 16;  // ints per ring slot (64 B)
 
 // ---- dispatch over (equation, network shape)
 struct Launch {

@@ -380,7 +380,9 @@ int dpi_problem_destroy(dpi_problem p) {
   return 0;
 }
 
-// The net's sticky status word (DPI_STATUS_*), zeroed; and whether every parameter is finite.
+// The net's ring of sticky status words (DPI_STATUS_*), zeroed, in host-visible memory the kernels
+// write with a vector store and the host reads without a HIP call; and whether every parameter is
+// finite.
 static int net_init_status(dpi_net_s* n, const float* params, size_t n_params) {
   n->finite = true;
   for (size_t i = 0; i < n_params; ++i)
@@ -388,9 +390,20 @@ static int net_init_status(dpi_net_s* n, const float* params, size_t n_params) {
       n->finite = false;
       break;
     }
-  HIPCHK(hipMalloc(&n->status, 256));
-  HIPCHK(hipMemset(n->status, 0, 256));
+  const size_t bytes = (size_t)DPI_STATUS_SLOTS * STATUS_STRIDE * sizeof(int);
+  void* h = nullptr;
+  HIPCHK(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h, 0, bytes);
+  n->status_host = (int*)h;
+  void* d = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&d, h, 0));
+  n->status = (int*)d;
+  n->slot = 0;
   return 0;
+}
+
+static volatile int* status_word(dpi_net net, int slot) {
+  return (volatile int*)(net->status_host + (size_t)slot * STATUS_STRIDE);
 }
 
 int dpi_net_create_zero(dpi_net* out) {
@@ -410,14 +423,27 @@ int dpi_net_set_precision(dpi_net net, int mode) {
 
 int dpi_net_status(dpi_net net, int clear, void* stream, int* status) {
   if (!net || !status) return fail(DPI_ERR_ARG, "net_status: bad arguments");
-  hipStream_t st = (hipStream_t)stream;
   int v = 0;
-  if (net->status) {
-    HIPCHK(hipMemcpyAsync(&v, net->status, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (clear && v) HIPCHK(hipMemsetAsync(net->status, 0, sizeof(int), st));
+  if (net->status_host) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    v = *status_word(net, net->slot);
+    if (clear && v) *status_word(net, net->slot) = 0;
   }
   *status = v;
+  return 0;
+}
+
+int dpi_net_status_slot(dpi_net net, int slot, int clear) {
+  if (!net || slot < 0 || slot >= DPI_STATUS_SLOTS) return fail(DPI_ERR_ARG, "net_status_slot: bad arguments");
+  net->slot = slot;
+  if (clear && net->status_host) *status_word(net, slot) = 0;
+  return 0;
+}
+
+int dpi_net_status_peek(dpi_net net, int slot, int* status) {
+  if (!net || !status || slot < 0 || slot >= DPI_STATUS_SLOTS)
+    return fail(DPI_ERR_ARG, "net_status_peek: bad arguments");
+  *status = net->status_host ? *status_word(net, slot) : 0;
   return 0;
 }
 
@@ -777,7 +803,7 @@ int dpi_net_destroy(dpi_net net) {
   if (!net) return 0;
   prep_tags_drop(net);
   if (net->blob) (void)hipFree(net->blob);
-  if (net->status) (void)hipFree(net->status);
+  if (net->status_host) (void)hipHostFree(net->status_host);
   delete net;
   return 0;
 }
@@ -888,7 +914,9 @@ static int gemm_mode() {
 static int net_mode(dpi_net net) { return (net && net->precision >= 0) ? net->precision : gemm_mode(); }
 static bool mlp_split(dpi_net net) { return net_mode(net) != DPI_GEMM_F32; }
 static bool pis_x3(dpi_net net) { return net_mode(net) != DPI_GEMM_F32; }
-static int* net_status(dpi_net net) { return (net && net->finite) ? net->status : nullptr; }
+static int* net_status(dpi_net net) {
+  return (net && net->finite && net->status) ? net->status + (size_t)net->slot * STATUS_STRIDE : nullptr;
+}
 
 extern "C" int dpi_set_gemm_precision(int mode) {
   if (mode != DPI_GEMM_F32 && mode != DPI_GEMM_F16X3 && mode != DPI_GEMM_AUTO)
@@ -1334,6 +1362,26 @@ static int pis_paths(dpi_problem p, dpi_net net, const float* tx, int n, int K, 
   return 0;
 }
 
+// The fused reduce (k_paths' last block per point) counts blocks on per-point tickets that the
+// baseline launch zeroes and the last block resets.  The host records which workspaces had a
+// baseline of how many points enqueued on them, and a fused label call on a workspace without one
+// fails instead of running a reduce whose tickets hold garbage (it would never fire and leave the
+// labels unwritten).
+static std::mutex g_base_mu;
+static std::unordered_map<const void*, int>& base_tags() {
+  static std::unordered_map<const void*, int> m;
+  return m;
+}
+static void base_tag_set(const void* ws, int n) {
+  std::lock_guard<std::mutex> g(g_base_mu);
+  base_tags()[ws] = n;
+}
+static bool base_tag_ok(const void* ws, int n) {
+  std::lock_guard<std::mutex> g(g_base_mu);
+  auto it = base_tags().find(ws);
+  return it != base_tags().end() && it->second == n;
+}
+
 int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void* ws, size_t ws_bytes, void* stream) {
   int rc = check_pair(p, net);
   if (rc) return rc;
@@ -1348,6 +1396,7 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
   q.tickets = (int*)(b + w.tk);
   if (!dispatch_any(p, net, q)) return fail(DPI_ERR_UNSUPPORTED, "point_baseline: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
+  base_tag_set(ws, n);
   return 0;
 }
 
@@ -1426,6 +1475,9 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
     if (nbp <= 64 && fused_reduce_on()) {  // k_paths' last block per point reduces and finalizes
+      if (!base_tag_ok(ws, n))
+        return fail(DPI_ERR_ARG, "label_moments: no dpi_point_baseline / dpi_sample_points_baseline of these n points "
+                                 "was enqueued on this workspace (the fused reduce's tickets are zeroed there)");
       a.tickets = (int*)(b + w.tk);
       a.rd_moments = moments;
       a.rd_y = y;
@@ -1499,6 +1551,7 @@ int dpi_sample_points_baseline(dpi_problem p, dpi_net net, int n, uint64_t seed,
   if (!dispatch_any(p, net, q))
     return fail(DPI_ERR_UNSUPPORTED, "sample_points_baseline: unsupported equation/network shape");
   HIPCHK(hipGetLastError());
+  base_tag_set(ws, n);
   return 0;
 }
 

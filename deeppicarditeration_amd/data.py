@@ -46,6 +46,143 @@ class SplitRangeWarning(RuntimeWarning):
     generator's later calls made, with exact-fp32 MFMA (DPI_GEMM_F32) for that network."""
 
 
+# include/dpi.h status ring: slot 0 serves the immediate (per-call) check, UNCHECKED_SLOT collects the
+# flags of calls made with range_check off (never read), the others are handed to RangeGroups
+IMMEDIATE_SLOT = 0
+UNCHECKED_SLOT = _lib.DPI_STATUS_SLOTS - 1
+
+
+class RangeGroup:
+    """The range guard of a group of label calls, checked once for the whole group instead of with
+    a stream synchronisation per call (include/dpi.h dpi_net_status_slot / _peek).
+
+    Every call run through the group is enqueued with the group's own slot of the net's
+    host-visible status ring selected, so its reductions flag into that slot and nowhere else.
+    `close()` records an event after the group's last call; `verify()` waits for that event — by
+    then the caller has usually enqueued the next group, so the GPU does not idle — reads the slot
+    from host memory and, if a label came out non-finite, switches the net to exact fp32 and
+    recomputes every registered call of the group (same points, same counters) into the tensors
+    it returned: the labels are final once verify() has returned, and a consumer that reads them
+    only after that never sees an unguarded label (IterableDatasetWithInternalBatch yields a buffer
+    only after its group verified; runner.LabelBuffer and bench.py verify before they use them).
+    A flag in exact fp32 raises DPIError, as the per-call guard does.  Multi-rank callers pass
+    `reduce_flag` (ShardedLabeler): the flag is MAX-reduced over the ranks, so every rank repairs
+    the same calls.  The reference's call (picard/data.py:211-223) has no such check: it computes
+    in fp64, where the fp16 split cannot overflow."""
+
+    def __init__(self, gen, slot):
+        self.gen = gen
+        self.slot = slot
+        self.calls = []  # (repair callable, returned output) in call order
+        self.reduce_flag = None
+        self.event = None
+        self.open = True
+        self.done = False
+
+    def run(self, fn):
+        """Enqueue fn() with this group's slot selected (no registration)."""
+        gen = self.gen
+        prev = gen._slot
+        gen._select_slot(self.slot)
+        try:
+            return fn()
+        finally:
+            gen._select_slot(prev)
+
+    def register(self, repair, out, reduce_flag=None):
+        """`out` (a tensor or a tuple of tensors) is final after verify(); repair() recomputes it."""
+        if self.done:
+            raise RuntimeError("RangeGroup.register() after verify()")
+        self.calls.append((repair, out))
+        if reduce_flag is not None:
+            self.reduce_flag = reduce_flag
+        return out
+
+    def enqueue(self, call, reduce_flag=None):
+        return self.register(call, self.run(call), reduce_flag)
+
+    def close(self):
+        """End of the group's enqueueing: an event after its last call on the current stream."""
+        if self.open:
+            self.open = False
+            if self.gen._scope is self:
+                self.gen._scope = None
+            self.event = torch.cuda.Event()
+            self.event.record(torch.cuda.current_stream(self.gen.device))
+
+    def verify(self):
+        """Wait for the group's work, check its slot, repair its calls if flagged; returns the flag."""
+        if self.done:
+            return 0
+        self.close()
+        self.event.synchronize()
+        st = _lib.c_int(0)
+        _lib.check(self.gen.lib.dpi_net_status_peek(self.gen.net.handle, self.slot, _lib.ctypes.byref(st)),
+                   "dpi_net_status_peek")
+        flag = st.value
+        if self.reduce_flag is not None:
+            flag = self.reduce_flag(flag)
+        self.done = True
+        self.gen._release_slot(self.slot)
+        if flag & _lib.DPI_STATUS_NONFINITE:
+            self.gen._repair(self.calls, self.reduce_flag)
+        self.calls = []
+        return flag
+
+    def discard(self):
+        """Give the slot back without checking (the group's outputs are dropped unread)."""
+        if not self.done:
+            self.close()
+            self.event.synchronize()
+            self.done = True
+            self.calls = []
+            self.gen._release_slot(self.slot)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+class _NoGroup:
+    """What deferred_range_check() returns with range_check off: runs calls unchecked."""
+    calls = ()
+
+    def run(self, fn):
+        return fn()
+
+    def register(self, repair, out, reduce_flag=None):
+        return out
+
+    def enqueue(self, call, reduce_flag=None):
+        return call()
+
+    def close(self):
+        pass
+
+    def verify(self):
+        return 0
+
+    def discard(self):
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def _copy_into(dst, src):
+    if isinstance(dst, (tuple, list)):
+        for d, s_ in zip(dst, src):
+            _copy_into(d, s_)
+    elif isinstance(dst, torch.Tensor) and dst is not src:
+        dst.copy_(src)
+
+
 def _hessian_approximation(cfg):
     """DATA.HESSIAN_APPROXIMATION ({method, kwargs: {v}}; config.py:99-101) -> (method, v)."""
     if cfg is None:
@@ -124,8 +261,13 @@ class OnlineDataGenerator:
         # status word says whether a label came out non-finite from finite weights — the network
         # evaluation overflowed fp16 (split storage) or fp32.  Split: the call is recomputed in
         # exact fp32 and the net stays fp32 (SplitRangeWarning); fp32 already: DPIError.  Never a
-        # silent inf / NaN label.  One stream synchronisation per call; False skips the check.
-        self.range_check = True
+        # silent inf / NaN label.  A direct call is checked at once (one stream synchronisation);
+        # calls inside deferred_range_check() — the label buffers of the dataset surface, picard train
+        # and bench.py — are checked once per group, one group behind (RangeGroup).  False skips it.
+        self._range_check = True
+        self._slot = IMMEDIATE_SLOT
+        self._scope = None  # the RangeGroup that label calls are deferred into (deferred_range_check)
+        self._free_slots = list(range(UNCHECKED_SLOT - 1, IMMEDIATE_SLOT, -1))
         self._fp32_fallback = False
         # Points per generator call of the dataset surface (None: unbounded).  The reference sizes
         # its calls by probing GPU memory (picard/memory.py:95-171): a dataset whose calls exceed
@@ -138,6 +280,55 @@ class OnlineDataGenerator:
         if label_dtype not in (torch.float32, torch.float64):
             raise ValueError(f"label_dtype must be float32 or float64 (got {label_dtype})")
         self.label_dtype = label_dtype
+
+    @property
+    def range_check(self):
+        return self._range_check
+
+    @range_check.setter
+    def range_check(self, on):
+        self._range_check = bool(on)
+        if self._scope is None:
+            self._select_slot(IMMEDIATE_SLOT if self._range_check else UNCHECKED_SLOT)
+
+    def _select_slot(self, slot, clear=False):
+        if slot != self._slot or clear:
+            _lib.check(self.lib.dpi_net_status_slot(self.net.handle, slot, 1 if clear else 0), "dpi_net_status_slot")
+            self._slot = slot
+
+    def _release_slot(self, slot):
+        self._free_slots.append(slot)
+
+    def deferred_range_check(self):
+        """A RangeGroup that this generator's guarded label calls are deferred into until it is
+        closed (use as a context manager, or call close()); verify() it before reading its labels.
+        Groups may be closed and still pending while the next one is open (one-ahead pipelines)."""
+        if not self._range_check or torch.cuda.is_current_stream_capturing():
+            return _NoGroup()
+        if self._scope is not None:
+            raise RuntimeError("deferred_range_check(): a group is already open on this generator")
+        if not self._free_slots:
+            raise RuntimeError(f"deferred_range_check(): all {UNCHECKED_SLOT - 1} status slots belong to groups that "
+                               "were not verified")
+        slot = self._free_slots.pop()
+        _lib.check(self.lib.dpi_net_status_slot(self.net.handle, slot, 1), "dpi_net_status_slot")
+        _lib.check(self.lib.dpi_net_status_slot(self.net.handle, self._slot, 0), "dpi_net_status_slot")
+        g = RangeGroup(self, slot)
+        self._scope = g
+        return g
+
+    def _repair(self, calls, reduce_flag=None):
+        """A group's label came out non-finite: exact fp32 for this net, then every registered call
+        again (same points and counters, each checked at once — a call that overflows fp32 too raises
+        DPIError) into the outputs it returned.  A group may hold calls enqueued in split mode before
+        an earlier group's repair switched the net, so fp32 here only means "from now on"."""
+        if not self._fp32_fallback:
+            warnings.warn("the fp16-split evaluation of this network left fp16's range (|activation| > 65504); its "
+                          "labels are recomputed, and this generator's later calls run, with exact-fp32 MFMA",
+                          SplitRangeWarning, stacklevel=3)
+            self.use_fp32()
+        for repair, out in calls:
+            _copy_into(out, self._guarded(repair, reduce_flag, defer=False))
 
     def __getstate__(self):
         # DataLoader worker processes (DATA.N_WORKERS > 0, picard/data.py:1768-1779) would pickle the
@@ -203,10 +394,9 @@ class OnlineDataGenerator:
         MT, MI = self.n_estimate_terminal, self.n_estimate_integral
         if MT == MI and MT <= PATHS_PER_CALL_MAX:
             pb = self._take_points(n_batch)
-            tx, y = self._guarded(lambda: self.sample_generate(n_batch, pb))
-            return self._out(tx, y)
+            return self._guarded(lambda: self._out(*self.sample_generate(n_batch, pb)))
         tx, pb = self.sample_t_and_x(n_batch)
-        return self._out(tx, self._generate(tx, pb, _lib.DPI_BOTH))
+        return self._guarded(lambda: self._out(tx, self._generate_once(tx, pb, _lib.DPI_BOTH)))
 
     def sample_generate(self, n_batch, point_base, bound=None, on_moments_begin=None, on_moments_end=None):
         """Points at counters [point_base, point_base + n) and their clipped labels (no range guard):
@@ -240,7 +430,7 @@ class OnlineDataGenerator:
     def sample_with_gradients_and_hessians(self, n_batch):
         """data.py:225-237: (tx, clip(u_ux_uxx)) with u_ux_uxx (n, 1 + nx + nx^2)."""
         tx, pb = self.sample_t_and_x(n_batch)
-        return self._out(tx, self._generate_hess(tx, pb, self.sample_bound))
+        return self._guarded(lambda: self._out(tx, self._generate_hess_once(tx, pb, self.sample_bound)))
 
     def generate_with_gradients_and_hessians(self, tx, point_base=None):
         """data.py:1220-1223: Malliavin-weight Hessian labels (no clip), (n, 1 + nx + nx^2)."""
@@ -305,8 +495,9 @@ class OnlineDataGenerator:
         return self._out(tx, torch.cat([u.to(tx), ux.to(tx), uh.reshape(u.shape[0], -1).to(tx)], -1))
 
     # ------------------------------------------------------------------ datasets (data.py:285-335)
-    def _dataset(self, n_total, n_batch_buffer, batch_size, sampler):
-        ds = IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, sampler)
+    def _dataset(self, n_total, n_batch_buffer, batch_size, sampler, guard=True):
+        ds = IterableDatasetWithInternalBatch(n_total, n_batch_buffer, batch_size, sampler,
+                                              range_guard=self if guard else None)
         cap = self.max_points_per_call
         if cap is not None and ds._n_samples_each_call > cap:
             raise torch.cuda.OutOfMemoryError(
@@ -325,13 +516,13 @@ class OnlineDataGenerator:
         return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_with_gradients_and_hessians)
 
     def dataset_exact(self, n_total, n_batch_buffer, batch_size):
-        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact, guard=False)
 
     def dataset_exact_with_gradients(self, n_total, n_batch_buffer, batch_size):
-        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients, guard=False)
 
     def dataset_exact_with_gradients_and_hessians(self, n_total, n_batch_buffer, batch_size):
-        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients_and_hessians)
+        return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients_and_hessians, guard=False)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
     def workspace_bytes(self, n, M, hessians=False):
@@ -457,17 +648,34 @@ class OnlineDataGenerator:
 
     # ------------------------------------------------------------------ internals
     def range_status(self, clear=True):
-        """DPI_STATUS_* bits set by the label calls on this generator's net since the last clear."""
+        """DPI_STATUS_* bits of the selected status slot (the immediate one outside a group) set by the
+        label calls on this generator's net since the last clear (synchronises the stream)."""
         return self.net.status(_stream(self._device), clear)
 
-    def _guarded(self, call):
-        """Run a label call; on a DPI_STATUS_NONFINITE flag switch the net to exact fp32 and run it
-        again (same points and counters), or raise if it already ran in fp32."""
-        y = call()
+    def _guarded(self, call, reduce_flag=None, defer=True):
+        """Run a label call under the range guard.  Inside deferred_range_check() the call is
+        registered with the open RangeGroup (checked at its verify()); otherwise it runs with the
+        immediate slot selected and is checked at once: on a DPI_STATUS_NONFINITE flag the net
+        switches to exact fp32 and the call runs again (same points and counters), or DPIError if
+        it already ran in fp32.  reduce_flag: the multi-rank MAX of a flag (ShardedLabeler)."""
+        if not self._range_check:
+            return call()
         # no check inside a hipGraph capture (a synchronisation there would invalidate the capture);
         # the flag stays set and the next checked call on this net reports it
-        if not self.range_check or torch.cuda.is_current_stream_capturing() or \
-                not (self.range_status() & _lib.DPI_STATUS_NONFINITE):
+        if torch.cuda.is_current_stream_capturing():
+            return call()
+        if defer and self._scope is not None:
+            return self._scope.enqueue(call, reduce_flag)
+        prev = self._slot
+        self._select_slot(IMMEDIATE_SLOT)
+        try:
+            y = call()
+            flag = self.range_status()
+        finally:
+            self._select_slot(prev)
+        if reduce_flag is not None:
+            flag = reduce_flag(flag)
+        if not flag & _lib.DPI_STATUS_NONFINITE:
             return y
         if self._fp32_fallback:
             raise _lib.DPIError("label call gave non-finite labels from a network with finite parameters in exact "
@@ -476,7 +684,7 @@ class OnlineDataGenerator:
                       "labels are recomputed, and this generator's later calls run, with exact-fp32 MFMA",
                       SplitRangeWarning, stacklevel=3)
         self.use_fp32()
-        return self._guarded(call)
+        return self._guarded(call, reduce_flag, defer=False)
 
     def use_fp32(self):
         """Evaluate this generator's network with exact-fp32 MFMA from now on (dpi_net_set_precision)."""

@@ -114,10 +114,18 @@ def buffer_plan(n_batch_buffer: Union[int, float], batch_size: int) -> Tuple[int
 class IterableDatasetWithInternalBatch(IterableDataset):
     """picard/dataset.py:20-137: yields `batch_size`-row batches cut from buffers, each buffer made
     by `batch_data_generator(n) -> (x (n, ·), y (n, ·))` calls.  Use with `DataLoader(batch_size=None)`.
-    `n` must be a multiple of the samples per buffer."""
+    `n` must be a multiple of the samples per buffer.
 
-    def __init__(self, n: int, n_batch_buffer: Union[int, float], batch_size: int, batch_data_generator):
+    `range_guard` (the OnlineDataGenerator whose label calls fill the buffers): each buffer's calls
+    run in one of its RangeGroups, and buffer k is yielded (and saved) only after its group
+    verified, which happens once buffer k+1's calls are enqueued — so the check waits on work the
+    GPU finished while it already runs the next buffer, instead of synchronising after every call.
+    The buffers are drawn in the same order either way (buffer k+1 is drawn one buffer earlier)."""
+
+    def __init__(self, n: int, n_batch_buffer: Union[int, float], batch_size: int, batch_data_generator,
+                 range_guard=None):
         super().__init__()
+        self.range_guard = range_guard
         (self.n_batch_buffer, self.n_samples_each_buffer, self._n_calls_to_generator_each_buffer,
          self._n_samples_each_call) = buffer_plan(n_batch_buffer, batch_size)
         self.batch_size = int(batch_size)
@@ -140,26 +148,54 @@ class IterableDatasetWithInternalBatch(IterableDataset):
             raise AssertionError("Saver can only be attached once")
         self.saver = saver
 
-    def refresh_buffer(self):
-        """One buffer: the generator calls' rows concatenated in call order (:110-118)."""
+    def _calls(self):
         xs, ys = [], []
         for _ in range(self._n_calls_to_generator_each_buffer):
             x, y = self.batch_data_generator(self._n_samples_each_call)[:2]
             xs.append(x)
             ys.append(y)
+        return xs, ys
+
+    @staticmethod
+    def _joined(xs, ys):
         if len(xs) == 1:
             return xs[0], ys[0]
         return torch.cat(xs, 0), torch.cat(ys, 0)
 
+    def refresh_buffer(self):
+        """One buffer: the generator calls' rows concatenated in call order (:110-118)."""
+        return self._joined(*self._calls())
+
+    def _emit(self, x, y):
+        if self.saver is not None:
+            self.saver.save((x, y), self.n_samples_each_buffer)
+        x = x.view(self.n_batch_buffer, self.batch_size, -1)
+        y = y.view(self.n_batch_buffer, self.batch_size, -1)
+        for b in range(self.n_batch_buffer):
+            yield x[b], y[b]
+
     def __iter__(self):
-        for _ in range(self.n_buffer_refresh):
-            x, y = self.refresh_buffer()
-            if self.saver is not None:
-                self.saver.save((x, y), self.n_samples_each_buffer)
-            x = x.view(self.n_batch_buffer, self.batch_size, -1)
-            y = y.view(self.n_batch_buffer, self.batch_size, -1)
-            for b in range(self.n_batch_buffer):
-                yield x[b], y[b]
+        if self.range_guard is None:
+            for _ in range(self.n_buffer_refresh):
+                yield from self._emit(*self.refresh_buffer())
+        else:
+            pending = None  # (group, xs, ys) of the buffer drawn but not yet verified
+            try:
+                for _ in range(self.n_buffer_refresh):
+                    with self.range_guard.deferred_range_check() as grp:
+                        xs, ys = self._calls()
+                    if pending is not None:
+                        (g, pxs, pys), pending = pending, None
+                        g.verify()  # joined after the check: a repair writes the calls' own outputs
+                        yield from self._emit(*self._joined(pxs, pys))
+                    pending = (grp, xs, ys)
+                if pending is not None:
+                    (g, pxs, pys), pending = pending, None
+                    g.verify()
+                    yield from self._emit(*self._joined(pxs, pys))
+            finally:
+                if pending is not None:  # iteration abandoned: the drawn buffer is dropped unread
+                    pending[0].discard()
         if self.saver is not None:
             self.saver.close()
 

@@ -35,22 +35,34 @@ from .solution import PISGradNet, ZeroSolution, construct_mlp
 class LabelBuffer:
     """Device-resident (tx, y) label store for one Picard iteration, filled by DATA_SIZE / POINTS_PER_CALL
     calls of a batch_data_generator `sample(n) -> (tx, y)` (a generator's sample_with_gradients /
-    sample_with_gradients_and_hessians / sample_exact_*, or a ShardedLabeler's)."""
+    sample_with_gradients_and_hessians / sample_exact_*, or a ShardedLabeler's).
 
-    def __init__(self, sample, n_total, points_per_call):
+    `guard` (the OnlineDataGenerator behind `sample`): the calls of one fill form one RangeGroup of
+    its range guard, checked once when the fill is done (data.RangeGroup) instead of with a stream
+    synchronisation after every call."""
+
+    def __init__(self, sample, n_total, points_per_call, guard=None):
         self.sample = sample
         self.n_total = int(n_total)
         self.ppc = max(1, min(int(points_per_call), self.n_total))
+        self.guard = guard
 
     def fill(self):
         txs, ys = [], []
         done = 0
-        while done < self.n_total:
-            n = min(self.ppc, self.n_total - done)
-            tx, y = self.sample(n)
-            txs.append(tx)
-            ys.append(y)
-            done += n
+        grp = self.guard.deferred_range_check() if hasattr(self.guard, "deferred_range_check") else None
+        try:
+            while done < self.n_total:
+                n = min(self.ppc, self.n_total - done)
+                tx, y = self.sample(n)
+                txs.append(tx)
+                ys.append(y)
+                done += n
+        finally:
+            if grp is not None:
+                grp.close()
+        if grp is not None:
+            grp.verify()  # before the concatenation: a repair rewrites the calls' own outputs
         return torch.cat(txs), torch.cat(ys)
 
 
@@ -173,7 +185,7 @@ class PicardRunner:
     def labels(self):
         gen = self.make_generator(self.u_current)
         d = self.cfg.DATA
-        return LabelBuffer(self.label_sampler(gen), d.DATA_SIZE, d.POINTS_PER_CALL).fill()
+        return LabelBuffer(self.label_sampler(gen), d.DATA_SIZE, d.POINTS_PER_CALL, guard=gen).fill()
 
     # ------------------------------------------------------------------ fit
     def fit(self, net, tx, y):

@@ -29,8 +29,11 @@ class ShardedLabeler:
         """sample_ahead (PISGradNet, prepare()): each prepare() also samples the NEXT batch's points,
         on a stream of their own, so the next prepare's rollout does not wait for a sampling launch
         on the side stream's critical path.  The batches get the same point ranges in the same
-        order (under the generator's seed and epoch at the prepare() that samples them); the points
-        sampled ahead of the last prepare() are skipped."""
+        order (under the generator's seed and epoch at the prepare() that samples them; a batch
+        sampled ahead under another seed or epoch than the next prepare()'s is dropped and that
+        prepare samples afresh); the points sampled ahead of the last prepare() are skipped — the
+        generator's point counter stays one batch further on, which later draws see as a shift of
+        their point indices."""
         self.gen = gen
         self.rank = rank
         self.world = world
@@ -72,31 +75,22 @@ class ShardedLabeler:
         dist.all_gather_into_tensor(flat, x, group=self.group)
         return self.gen.sums_reduce(flat.view((self.world,) + tuple(x.shape)))
 
+    def _reduce_flag(self, flag):
+        """A range-guard flag of this rank -> the MAX over all ranks (every rank repairs together)."""
+        if self.world == 1:
+            return flag
+        import torch.distributed as dist
+        dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.gen.device
+        t = torch.tensor([float(flag)], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
     def _guarded(self, call):
         """The generator's range guard (OnlineDataGenerator._guarded) across ranks: any rank's flag
-        is every rank's (a one-word all-reduce), so all ranks recompute in fp32 together."""
-        gen = self.gen
-        y = call()
-        if not getattr(gen, "range_check", False) or torch.cuda.is_current_stream_capturing():
-            return y
-        flag = gen.range_status()
-        if self.world > 1:
-            import torch.distributed as dist
-            dev = (y[-1] if isinstance(y, tuple) else y).device
-            t = torch.tensor([float(flag)], device=dev if dist.get_backend(self.group) != "gloo" else "cpu")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            flag = int(t.item())
-        if not flag:
-            return y
-        from . import _lib
-        if gen._fp32_fallback:
-            raise _lib.DPIError("non-finite labels from a network with finite parameters in exact fp32")
-        import warnings
-        from .data import SplitRangeWarning
-        warnings.warn("the fp16-split evaluation left fp16's range: labels recomputed in exact fp32", SplitRangeWarning,
-                      stacklevel=3)
-        gen.use_fp32()
-        return self._guarded(call)
+        is every rank's (a one-word MAX all-reduce), so all ranks recompute in fp32 together; inside
+        the generator's deferred_range_check() the call joins the open RangeGroup."""
+        g = getattr(self.gen, "_guarded", None)
+        return call() if g is None else g(call, reduce_flag=self._reduce_flag)
 
     def labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
         return self._guarded(lambda: self._labels_hessians(tx, point_base, on_moments_begin, on_moments_end))
@@ -144,13 +138,13 @@ class ShardedLabeler:
         # PISGradNet only: its points need no workspace (the baseline lives in the label call)
         pis = str(getattr(getattr(gen, "net", None), "desc", "")).startswith("pisgrad")
         ahead, self._ahead = self._ahead, None
-        if ahead is not None and ahead[0] != n:
-            ahead = None  # another batch size: those points are skipped
+        if ahead is not None and ahead[:3] != (n, getattr(gen, "seed", None), getattr(gen, "epoch", None)):
+            ahead = None  # another batch size, seed or epoch (Picard iteration): those points are skipped
         with torch.cuda.stream(self._side):
             if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
                 self._side.wait_event(self._prep_free[k])
             if ahead is not None:
-                _, tx, pb, ev = ahead
+                tx, pb, ev = ahead[3:]
                 self._side.wait_event(ev)
                 tx.record_stream(self._side)
             elif hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
@@ -172,7 +166,7 @@ class ShardedLabeler:
                 tx2, _ = gen.sample_t_and_x(n, point_base=pb2)
                 ev2 = torch.cuda.Event()
                 ev2.record(self._samp)
-            self._ahead = (n, tx2, pb2, ev2)
+            self._ahead = (n, getattr(gen, "seed", None), getattr(gen, "epoch", None), tx2, pb2, ev2)
         return tx, pb, ws, ready, k, flags
 
     def begin(self, tx=None, point_base=None, flags=None, on_moments_begin=None, on_moments_end=None,
@@ -187,10 +181,7 @@ class ShardedLabeler:
             raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
         slot = wslot = None
         kflags = None
-        if not self._pipeline_pending():
-            # a pipeline starts: the range-status word must describe only its own batches
-            # (pipeline_range_check reads it once the pipeline is drained)
-            self._clear_range_status()
+        grp = self._range_group()
         if prepared is not None:
             tx, point_base, ws, ready, slot, pflags = prepared
             if flags is not None and flags != pflags:
@@ -216,57 +207,63 @@ class ShardedLabeler:
             self.gen.point_baseline(tx, ws=ws)
         flags = _lib.DPI_BOTH if flags is None else flags
         m0, m1 = self.shard(M)
+        repair = (tx, point_base, flags)  # end() registers labels(tx, point_base, flags) as the repair
         if on_moments_begin:
             on_moments_begin()
         if self.world == 1:  # one rank: the labels come out of the moments' reduce launch
-            y, _ = self.gen.label_moments_finalize(tx, point_base, M, flags if kflags is None else kflags, ws)
+            y, _ = grp.run(lambda: self.gen.label_moments_finalize(tx, point_base, M,
+                                                                   flags if kflags is None else kflags, ws))
             if on_moments_end:
                 on_moments_end()
-            return (None, y, None, None, flags, M, slot, wslot)  # ws None: y final (end() only recycles)
-        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags if kflags is None else kflags, ws)
+            return (None, y, None, None, flags, M, slot, wslot, grp, repair)  # ws None: y final (end() recycles)
+        mom = grp.run(lambda: self.gen.label_moments(tx, point_base, M, m0, m1, flags if kflags is None else kflags,
+                                                     ws))
         if on_moments_end:
             on_moments_end()
         import torch.distributed as dist
         mom = mom.contiguous()
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
         work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
-        return (ws, flat, work, tuple(mom.shape), flags, M, slot, wslot)
+        return (ws, flat, work, tuple(mom.shape), flags, M, slot, wslot, grp, repair)
 
     def _pipeline_pending(self):
         return any(getattr(self, "_ws_busy", ())) or any(getattr(self, "_prep_busy", ()))
 
-    def _clear_range_status(self):
+    def _range_group(self):
+        """The RangeGroup a pipelined batch's reductions flag into: the generator's open
+        deferred_range_check() group if there is one, else this labeler's pipeline group, opened by
+        the first begin() after the last check and verified by pipeline_range_check()."""
         gen = self.gen
-        if getattr(gen, "range_check", False) and hasattr(gen, "range_status") and \
-                not torch.cuda.is_current_stream_capturing():
-            gen.range_status(clear=True)
+        if not hasattr(gen, "deferred_range_check"):
+            from .data import _NoGroup
+            return _NoGroup()
+        if gen._scope is not None:
+            return gen._scope
+        pg = getattr(self, "_pipe_group", None)
+        if pg is None:
+            pg = gen.deferred_range_check()
+            if gen._scope is pg:  # not the open scope: begin() selects its slot around each enqueue
+                gen._scope = None
+            self._pipe_group = pg
+        return pg
 
     def pipeline_range_check(self):
-        """The range guard for the pipelined path (prepare/begin/end), which cannot recompute a
-        batch once later ones are in flight: after the last end(), read and clear the net's status
-        word (a MAX all-reduce across ranks, like labels()) and raise DPIError if any pipelined
-        batch gave non-finite sums — rerun those batches with labels(), which falls back to fp32."""
-        gen = self.gen
-        if not getattr(gen, "range_check", False) or not hasattr(gen, "range_status"):
-            return 0
+        """The range guard of the pipelined path (prepare/begin/end) outside a generator group:
+        once every pending batch has ended, verify the pipeline's RangeGroup (one event wait and a
+        host read of its status slot; a MAX across ranks) — a flagged pipeline has its batches
+        recomputed in exact fp32 into the labels end() returned (SplitRangeWarning), or raises
+        DPIError if the net already ran in fp32.  Returns the flag."""
         if self._pipeline_pending():
             raise RuntimeError("pipeline_range_check(): end() every pending batch first")
-        from . import _lib
-        flag = gen.range_status(clear=True)
-        if self.world > 1:
-            import torch.distributed as dist
-            dev = "cpu" if dist.get_backend(self.group) == "gloo" else gen.device
-            t = torch.tensor([float(flag)], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            flag = int(t.item())
-        if flag & _lib.DPI_STATUS_NONFINITE:
-            raise _lib.DPIError("pipelined labels (begin/end) gave non-finite sums: the fp16-split evaluation left "
-                                "fp16's range; recompute those batches with labels(), which falls back to exact fp32")
-        return flag
+        pg, self._pipe_group = getattr(self, "_pipe_group", None), None
+        if pg is None:
+            return 0
+        pg.reduce_flag = self._reduce_flag
+        return pg.verify()
 
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
-        ws, mom, work, shape, flags, M, slot, wslot = pending
+        ws, mom, work, shape, flags, M, slot, wslot, grp, (tx, point_base, rflags) = pending
         if ws is None:  # one rank: begin() already finalized
             y = mom
         else:
@@ -281,7 +278,8 @@ class ShardedLabeler:
             self._prep_busy[slot] = False
         if wslot is not None:  # stream order makes the next user of this workspace run after finalize
             self._ws_busy[wslot] = False
-        return y
+        # final once the group verifies: a flagged batch is recomputed by the unpipelined labels()
+        return grp.register(lambda: self._labels(tx, point_base, rflags), y, self._reduce_flag)
 
     def labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients for tx with this rank's MC shard; identical y on every rank

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 2
+#define DPI_ABI_VERSION 3
 
 /* error codes */
 #define DPI_OK 0
@@ -146,15 +146,32 @@ int dpi_set_gemm_precision(int mode);
 int dpi_net_set_precision(dpi_net net, int mode);
 
 /* Range guard.  Every label reduction of a call on `net` (dpi_label_moments*, the Hessian sums)
- * sets DPI_STATUS_NONFINITE in the net's sticky device status word when a label sum (not a sum of
+ * sets DPI_STATUS_NONFINITE in a sticky status word of the net when a label sum (not a sum of
  * squares, whose overflow leaves the labels intact) is not finite
  * while every parameter of the net is finite: the network evaluation overflowed its number format
  * (fp16's 65,504 in the fp16-split PISGradNet storage, or fp32's range), where the fp64 reference
  * would not.  (Non-finite parameters give non-finite labels as in the reference, unflagged.)
- * dpi_net_status copies the word to *status after the work queued on `stream` (a synchronisation)
- * and, with clear != 0, resets it.  Replaces no reference interface. */
+ *
+ * The words form a ring of DPI_STATUS_SLOTS slots in host-visible (fine-grained, pinned) memory,
+ * written by the kernels with a plain vector store.  A call flags into the slot that was selected
+ * when it was enqueued (dpi_net_status_slot; slot 0 at creation), so a caller can give a group of
+ * calls a slot of its own and read it once the group's work has completed (an event) with
+ * dpi_net_status_peek, which reads host memory and issues no HIP call: the range check of a label
+ * buffer costs no stream synchronisation of its own.
+ * dpi_net_status: the selected slot after the work queued on `stream` (a synchronisation) and,
+ * with clear != 0, resets it.  dpi_net_status_slot: select `slot` for the calls enqueued from now
+ * on and, with clear != 0, zero it first (a host store: no enqueued call may still flag into it).
+ * Zero networks have no status words: their reads return 0.  Replaces no reference interface. */
 #define DPI_STATUS_NONFINITE 1
+#define DPI_STATUS_SLOTS 64
 int dpi_net_status(dpi_net net, int clear, void* stream, int* status);
+int dpi_net_status_slot(dpi_net net, int slot, int clear);
+int dpi_net_status_peek(dpi_net net, int slot, int* status);
+
+/* Identity of this build: the SHA-256 (hex) of the sources and flags it was compiled from
+ * (deeppicarditeration_amd/build.py source_hash), NUL-terminated into buf; returns its length.
+ * The host layer refuses a library whose identity differs from the tree's sources. */
+int dpi_build_id(char* buf, size_t len);
 
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
 size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
@@ -182,7 +199,10 @@ int dpi_point_baseline(dpi_problem p, dpi_net net, const float* tx, int n, void*
  * contributions, [1] = sum of squares.  Summation order is fixed (pairwise over 64-path
  * blocks), so results are bit-reproducible; ranges aligned to power-of-two block counts
  * combine with dpi_moments_reduce bit-identically to a single call.  Requires
- * dpi_point_baseline on the same workspace first. */
+ * dpi_point_baseline (or dpi_sample_points_baseline) of the same n points on the same workspace
+ * first: for MLP / zero nets with <= 64 path blocks the label reduce runs inside the path launch,
+ * counting blocks on per-point tickets the baseline zeroes (and the last block resets), and the
+ * call fails with DPI_ERR_ARG on a workspace that had no such baseline enqueued. */
 int dpi_label_moments(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                       uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                       void* ws, size_t ws_bytes, void* stream);

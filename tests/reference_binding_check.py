@@ -81,6 +81,7 @@ def make_recording_generator(OnlineDataGenerator):
             self.n_estimate_integral = int(kw.get("n_estimate_integral", 1))
             self.point_base = 0
             self.calls = []
+            self._range_check = False  # no label kernels here, so no range guard (data.RangeGroup)
 
         def _rows(self, n, width):
             M = self.n_estimate_integral

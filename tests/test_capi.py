@@ -69,6 +69,13 @@ def test_host_side_argument_errors_without_gpu():
     assert lib.dpi_net_set_precision(None, 0) == _lib.DPI_ERR_ARG
     st = _lib.c_int(0)
     assert lib.dpi_net_status(None, 1, None, _lib.ctypes.byref(st)) == _lib.DPI_ERR_ARG
+    # the status ring: slot range checked; a zero net has no words (reads 0, host only)
+    assert lib.dpi_net_status_slot(n, _lib.DPI_STATUS_SLOTS, 1) == _lib.DPI_ERR_ARG
+    assert lib.dpi_net_status_slot(n, -1, 0) == _lib.DPI_ERR_ARG
+    assert lib.dpi_net_status_slot(n, 5, 1) == 0
+    st.value = 7
+    assert lib.dpi_net_status_peek(n, 5, _lib.ctypes.byref(st)) == 0 and st.value == 0
+    assert lib.dpi_net_status_peek(n, 64, _lib.ctypes.byref(st)) == _lib.DPI_ERR_ARG
     assert lib.dpi_net_destroy(n) == 0 and lib.dpi_problem_destroy(h) == 0
 
 
@@ -76,3 +83,24 @@ def test_product_fails_loudly_without_library(tmp_path, monkeypatch):
     from deeppicarditeration_amd import _lib
     with pytest.raises(_lib.DPIError):
         _lib.load(tmp_path / "missing.so")
+
+
+def test_library_is_built_from_this_tree():
+    """The .so embeds the SHA-256 of the sources it was built from (dpi_build_id); the in-tree
+    library must match the tree (build.needs_build compares the same hash, not mtimes)."""
+    from deeppicarditeration_amd import _lib, build as B
+    lib = _lib.load()
+    assert _lib.build_id(lib) == B.source_hash()
+    assert not B.needs_build()
+
+
+def test_load_refuses_a_library_built_from_other_sources(monkeypatch):
+    from deeppicarditeration_amd import _lib, build as B
+    lib = _lib.load()
+    monkeypatch.delenv("DPI_HIP_LIB", raising=False)
+    monkeypatch.setattr(B, "source_hash", lambda: "0" * 64)
+    with pytest.raises(_lib.DPIError, match="other sources"):
+        _lib.check_build_id(lib, B.OUT)
+    # an explicit DPI_HIP_LIB (an A/B variant) is the caller's choice: not checked
+    monkeypatch.setenv("DPI_HIP_LIB", str(B.OUT))
+    _lib.check_build_id(lib, B.OUT)

@@ -93,35 +93,6 @@ def test_generator_and_labeler_surfaces_use_the_two_launch_path():
     assert torch.equal(y_a, y_c) and torch.equal(y_b, y_c)
 
 
-@pytest.mark.parametrize("kind", ["pis", "cha"])
-def test_label_calls_write_nothing_past_the_workspace(kind):
-    """A partial last tile (3 points x 64 paths = 192 rows: one full 128-row tile and a half one)
-    must not store past the workspace:
-    a canary of 4 MB after dpi_workspace_bytes stays untouched (k_pis_net's row saves go through
-    per-tile buffer resources whose range check covers the whole row offset)."""
-    torch.manual_seed(0)
-    if kind == "pis":
-        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
-                                   alpha_scale=4.0)
-        net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=NX, g0=eq.g, T=1.0)
-    else:
-        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
-        net = dpi.construct_mlp(1 + NX, 1, [128] * 4, ["ELU"] * 4, None)
-    n, M = 3, 64
-    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=M,
-                                  n_estimate_integral=M, n_euler_steps=4, seed=5)
-    need = gen.workspace_bytes(n, M)
-    canary = 4 << 20
-    buf = torch.full((need + canary,), 0xA5, dtype=torch.uint8, device="cuda:0")
-    ws = buf[:need]
-    tx, pb = gen.sample_t_and_x(n, point_base=0)
-    gen.point_baseline(tx, ws=ws)
-    mom = gen.label_moments(tx, pb, M, 0, M, L.DPI_BOTH, ws)
-    torch.cuda.synchronize()
-    assert torch.isfinite(mom).all()
-    assert bool((buf[need:] == 0xA5).all())
-
-
 def test_prepare_with_points_sampled_ahead_equals_labels():
     """ShardedLabeler(sample_ahead=True) (PISGradNet, the bench's HJB schedule): every prepared batch
     gets the next consecutive point range, and its labels equal labels() on the same points."""
@@ -143,3 +114,40 @@ def test_prepare_with_points_sampled_ahead_equals_labels():
         tx0, _ = gen.sample_t_and_x(3, point_base=pb)
         assert torch.equal(tx, tx0)
         assert torch.equal(y, ref.labels(tx, pb))
+
+
+def test_points_sampled_ahead_under_another_epoch_are_dropped():
+    """A batch sampled ahead under the generator's previous epoch (a new Picard iteration reusing
+    the labeler) is not used: the next prepare() samples its points afresh under the new epoch."""
+    torch.manual_seed(0)
+    eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 2, dim=NX, g0=eq.g, T=1.0)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                  n_estimate_integral=64, n_euler_steps=2, seed=5)
+    lab = ShardedLabeler(gen, sample_ahead=True)
+    prep = lab.prepare(2)
+    lab.end(lab.begin(prepared=prep))
+    gen.epoch += 1
+    prep = lab.prepare(2)
+    tx, pb = prep[0], prep[1]
+    y = lab.end(lab.begin(prepared=prep))
+    tx0, _ = gen.sample_t_and_x(2, point_base=pb)
+    assert torch.equal(tx, tx0)
+    assert torch.equal(y, ShardedLabeler(gen).labels(tx, pb))
+
+
+def test_fused_label_call_without_a_baseline_on_its_workspace_fails():
+    """The fused reduce counts blocks on tickets the baseline launch zeroes: a label call on a
+    workspace no baseline of these points was enqueued on fails (DPI_ERR_ARG) instead of running a
+    reduce that never fires."""
+    gen = _make("cha", 256, 2)
+    tx, pb = gen.sample_t_and_x(3, point_base=0)
+    # an address no earlier workspace of this process started at (an odd offset into a fresh block)
+    odd = 7 * 4096 + 256
+    ws = torch.empty(gen.workspace_bytes(3, 256) + odd, dtype=torch.uint8, device="cuda:0")[odd:]
+    with pytest.raises(L.DPIError, match="baseline"):
+        gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, ws)
+    gen.point_baseline(tx, ws=ws)
+    y, _ = gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, ws)
+    assert torch.isfinite(y).all()

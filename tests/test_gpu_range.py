@@ -156,3 +156,110 @@ def test_weight_scaled_goldens_both_modes(mode, case):
     parts = rel_l2_parts(y, f["y"])
     print(case, mode, f"max|y| {np.abs(f['y']).max():.2e}", parts, "fp32 fallback:", gen._fp32_fallback)
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+# ---------------------------------------------------------------- the deferred guard (RangeGroup)
+def _fp32_twin(scale):
+    """The same generator state forced to exact fp32: what a repaired call must equal bit for bit."""
+    gen, _, _ = _pis(scale)
+    gen.use_fp32()
+    return gen
+
+
+def test_range_group_repairs_its_calls_in_place():
+    """Split-mode PISGradNet at 32x (fp16 overflow) inside deferred_range_check(): no stream
+    synchronisation per call, the non-finite labels sit in the returned tensors until verify(),
+    which warns, switches the net to fp32 and rewrites those tensors — equal to fp32 calls on the
+    same counters and within 1e-4 of the oracle."""
+    from deeppicarditeration_amd.data import SplitRangeWarning
+    gen, oeq, onet = _pis(32.0)
+    with gen.deferred_range_check() as grp:
+        tx1, y1 = gen.sample_with_gradients(2)
+        tx2, y2 = gen.sample_with_gradients(3)
+    with pytest.warns(SplitRangeWarning):
+        flag = grp.verify()
+    assert flag == 1 and gen._fp32_fallback
+    ref = _fp32_twin(32.0)
+    for tx, y in ((tx1, y1), (tx2, y2)):
+        txr, yr = ref.sample_with_gradients(tx.shape[0])
+        assert torch.equal(tx, txr) and torch.equal(y, yr)
+    o = O.labels_grad(oeq, onet, tx1.cpu().double().numpy(), 128, 10, 2, 1, 0)
+    y = y1.cpu().double().numpy()
+    assert _rel(y[:, :1], o[:, :1]) < TOL and _rel(y[:, 1:], o[:, 1:]) < TOL
+
+
+def test_range_group_without_overflow_changes_nothing():
+    """A group whose calls stay in range verifies to 0: no warning, labels bitwise the per-call
+    guarded ones, the net stays on the split MFMA."""
+    a, _, _ = _pis(1.0)
+    b, _, _ = _pis(1.0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        with a.deferred_range_check() as grp:
+            ya = [a.sample_with_gradients(2)[1] for _ in range(3)]
+        assert grp.verify() == 0
+    yb = [b.sample_with_gradients(2)[1] for _ in range(3)]
+    assert all(torch.equal(p, q) for p, q in zip(ya, yb)) and not a._fp32_fallback
+
+
+def test_dataset_surface_verifies_each_buffer_before_yielding_it():
+    """dataset_with_gradients (the boundary the reference's data module pulls from): every yielded
+    batch is finite and equals the fp32 labels, with one SplitRangeWarning, at no per-call sync."""
+    from deeppicarditeration_amd.data import SplitRangeWarning
+    gen, _, _ = _pis(32.0)
+    ds = gen.dataset_with_gradients(12, 1, 4)  # 3 buffers of one 4-point call each
+    with pytest.warns(SplitRangeWarning):
+        batches = list(ds)
+    ref = _fp32_twin(32.0)
+    for x, y in batches:
+        xr, yr = ref.sample_with_gradients(4)
+        assert torch.equal(x, xr) and torch.equal(y, yr)
+        assert torch.isfinite(y).all()
+
+
+def test_label_buffer_fill_is_one_range_group():
+    """picard train's LabelBuffer.fill: its calls form one group, checked once after the fill."""
+    from deeppicarditeration_amd.data import SplitRangeWarning
+    from deeppicarditeration_amd.runner import LabelBuffer
+    gen, _, _ = _pis(32.0)
+    with pytest.warns(SplitRangeWarning):
+        tx, y = LabelBuffer(gen.sample_with_gradients, 6, 2, guard=gen).fill()
+    ref = _fp32_twin(32.0)
+    txr, yr = LabelBuffer(ref.sample_with_gradients, 6, 2, guard=ref).fill()
+    assert torch.equal(tx, txr) and torch.equal(y, yr)
+
+
+def test_pipeline_flag_survives_a_later_begin():
+    """a flagged begin/end batch followed by another begin/end must still be caught by
+    pipeline_range_check() (begin() no longer clears the status; each pipeline has its own slot),
+    which repairs both batches' labels in place."""
+    from deeppicarditeration_amd.data import SplitRangeWarning
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    gen, _, _ = _pis(32.0)
+    lab = ShardedLabeler(gen)
+    out = []
+    for _ in range(2):
+        tx, pb = gen.sample_t_and_x(2)
+        out.append((tx, pb, lab.end(lab.begin(tx, pb))))
+    with pytest.warns(SplitRangeWarning):
+        assert lab.pipeline_range_check() == 1
+    for tx, pb, y in out:
+        assert torch.isfinite(y).all()
+        assert torch.equal(y, ShardedLabeler(gen).labels(tx, pb))  # the net is fp32 now
+
+
+def test_range_group_fp32_overflow_raises():
+    """Labels beyond fp32's range inside a group: verify() raises DPIError after the fp32 retry."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd._lib import DPIError
+    eq = dpi.Cha(100, 1.0, 5.0, 1.0)
+    torch.manual_seed(3)
+    net = _scaled(dpi.construct_mlp(101, 1, [32, 32], ["ELU"] * 2, None), 1e13)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                  n_estimate_integral=64, n_euler_steps=2, seed=1)
+    with gen.deferred_range_check() as grp:
+        gen.sample_with_gradients(2)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        with pytest.raises(DPIError, match="fp32"):
+            grp.verify()
