@@ -14,7 +14,7 @@ DPI_ABI_VERSION = 3
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
-DPI_ACT_ELU = 1
+DPI_ACT_ELU, DPI_ACT_TANH = 1, 2
 DPI_TERMINAL, DPI_INTEGRAL, DPI_BOTH = 1, 2, 3
 DPI_PREPARED = 4  # dpi_label_moments: dpi_label_prepare already ran with the same arguments
 DPI_PATH_BLOCK = 64

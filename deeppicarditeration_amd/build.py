@@ -1,7 +1,7 @@
 """Build libdpi_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
 
-Seven translation units (the C-ABI / PIS / reduce TU, one k_paths family per equation and one
-TD-estimator k_paths family per equation) compile in parallel to objects, then link into one
+Ten translation units (the C-ABI / PIS / reduce TU, one k_paths family per equation, one
+TD-estimator k_paths family per equation and one Tanh-activation family per equation) compile in parallel to objects, then link into one
 shared library together with a generated one-function unit, `dpi_build_id()`, that returns the
 SHA-256 of the sources and flags (`source_hash`).  The same hash goes into `libdpi_hip.so.buildid`
 beside the library: a build is current when that file matches the tree's hash (not by mtime), and
@@ -17,7 +17,8 @@ ROOT = Path(__file__).resolve().parent
 REPO = ROOT.parent
 CSRC = ROOT / "csrc"
 UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_gbm.hip", "dpi_paths_td_cha.hip",
-         "dpi_paths_td_ou.hip", "dpi_paths_td_gbm.hip"]
+         "dpi_paths_td_ou.hip", "dpi_paths_td_gbm.hip", "dpi_paths_cha_tanh.hip", "dpi_paths_ou_tanh.hip",
+         "dpi_paths_gbm_tanh.hip"]
 OBJ = ROOT / "build"
 OUT = ROOT / "libdpi_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -70,11 +71,11 @@ def build(force=False, verbose=True):
         obj = OBJ / (Path(u).stem + ".o")
         return force or not obj.exists() or obj.stat().st_mtime < max(newest_header, (CSRC / u).stat().st_mtime)
 
+    bid = source_hash()  # before compiling: a source edited during the build leaves the result stale
     todo = [u for u in UNITS if stale(u)]
     with ThreadPoolExecutor(max_workers=max(1, len(todo))) as ex:
         list(ex.map(compile_unit, todo))
     objs = [OBJ / (Path(u).stem + ".o") for u in UNITS]
-    bid = source_hash()
     objs.append(build_id_object(bid))
     tmp = OUT.with_name(OUT.name + ".tmp")
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]

@@ -69,6 +69,7 @@ constexpr int HMAX = 128;
 struct NetDev {
   int kind;  // 0 zero, 1 mlp
   int H, L, nxp;
+  int act;   // DPI_ACT_* of every hidden layer (k_paths: the ACT template parameter, k_baseline: read here)
   const float* W1x;   // (H, nxp)   W1[:, 1:]
   const float* w1t;   // (H)        W1[:, 0]
   const float* b1;    // (H)
@@ -97,6 +98,41 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 }
 __device__ __forceinline__ float elu(float z) { return z > 0.f ? z : __expf(z) - 1.0f; }
 __device__ __forceinline__ float delu_from_a(float a) { return a > 0.f ? 1.0f : a + 1.0f; }
+
+// tanh for the network activations (torch.nn.Tanh): 1 - 2 / (e^{2z} + 1) — v_exp_f32 + v_rcp_f32,
+// four VALU operations and no extra live registers; saturates to +-1 (e^{2z} = inf or 0).  Its error
+// is absolute (~1e-7 near z = 0, where 1 - x cancels), as is ELU's e^z - 1 on the same hardware.
+__device__ __forceinline__ float tanh_act(float z) {
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * z)), 1.0f);
+}
+
+// The MLP activations of construct_mlp (picard/solution.py:123-135) the kernels are compiled for:
+// f(z), and the first and second derivatives expressed through the activation value a = f(z)
+// (what the backward passes and the Hessian-diagonal sweeps hold).
+template <int ACT>
+struct Act;
+template <>
+struct Act<DPI_ACT_ELU> {  // ELU(alpha = 1)
+  static __device__ __forceinline__ float f(float z) { return elu(z); }
+  static __device__ __forceinline__ float d(float a) { return delu_from_a(a); }
+  static __device__ __forceinline__ float d2(float a) { return a > 0.f ? 0.f : a + 1.0f; }
+};
+template <>
+struct Act<DPI_ACT_TANH> {  // tanh' = 1 - a^2, tanh'' = -2 a (1 - a^2)
+  static __device__ __forceinline__ float f(float z) { return tanh_act(z); }
+  static __device__ __forceinline__ float d(float a) { return fmaf(-a, a, 1.0f); }
+  static __device__ __forceinline__ float d2(float a) { return -2.0f * a * fmaf(-a, a, 1.0f); }
+};
+// Runtime selection for the shape-generic, latency-bound per-point baseline (k_baseline).
+__device__ __forceinline__ float act_f(int act, float z) {
+  return act == DPI_ACT_TANH ? Act<DPI_ACT_TANH>::f(z) : Act<DPI_ACT_ELU>::f(z);
+}
+__device__ __forceinline__ float act_d(int act, float a) {
+  return act == DPI_ACT_TANH ? Act<DPI_ACT_TANH>::d(a) : Act<DPI_ACT_ELU>::d(a);
+}
+__device__ __forceinline__ float act_d2(int act, float a) {
+  return act == DPI_ACT_TANH ? Act<DPI_ACT_TANH>::d2(a) : Act<DPI_ACT_ELU>::d2(a);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -245,7 +281,7 @@ struct Lds {
 // cmul, vec[0:H] = base0 (layer-1 bias incl. W1x x), vec[H:2H] = w1t, vec[2H:3H] = wout,
 // vec[3H:4H] = c1, bh[l*H:(l+1)*H] = biases of hidden layers l >= 1.
 // If bx_out != nullptr (baseline mode) writes b1 + W1x S (per path) to bx_out[pp*bstride + h].
-template <int KIND, int H, int L, class SH>
+template <int KIND, int H, int L, int ACT, class SH>
 __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& sh, int nxt, float& u_out,
                                          float& gsum_out, float& gA_out, float& gB_out, float* bx_out,
                                          int bstride, int n_valid_paths) {
@@ -282,7 +318,7 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
         for (int r = 0; r < 4; ++r) {
           const int h = 16 * T + 4 * qq + r;
           const float z = fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h]));
-          act[0][T][r] = elu(z);
+          act[0][T][r] = Act<ACT>::f(z);
           if (bx_out && pp < n_valid_paths) bx_out[(size_t)pp * bstride + h] = sh.vec[h] + acc[r];
         }
       }
@@ -314,7 +350,7 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int h = 16 * T + 4 * qq + r;
-            act[l][T][r] = elu(acc[r] + sh.bh[l * H + h]);
+            act[l][T][r] = Act<ACT>::f(acc[r] + sh.bh[l * H + h]);
           }
         }
       }
@@ -329,7 +365,7 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
       const int h = 16 * T + 4 * qq + r;
       const float w = sh.vec[2 * H + h];
       up = fmaf(w, act[L - 1][T][r], up);
-      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+      act[L - 1][T][r] = w * Act<ACT>::d(act[L - 1][T][r]);
     }
   u_out = qsum(up) + net.bout;
   // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
@@ -356,7 +392,7 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
             acc = mfma4(a.w, act[l + 1][t][3], acc);
           }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) act[l][T][r] = acc[r] * delu_from_a(act[l][T][r]);
+          for (int r = 0; r < 4; ++r) act[l][T][r] = acc[r] * Act<ACT>::d(act[l][T][r]);
         }
       }
     }
@@ -473,7 +509,7 @@ struct SplitStream {
 // mlp_tile on the fp16-split MFMA (H % 32 == 0): same inputs, outputs and tile layout; each
 // 16x16x4 f32 chain becomes 16x16x32 f16 chunks (3 MFMAs per 32-wide chunk instead of 8), the
 // weights come pre-split from NetDev::*S, the activations are split in registers.
-template <int KIND, int H, int L, class SH>
+template <int KIND, int H, int L, int ACT, class SH>
 __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net, SH& sh, float& u_out,
                                                float& gsum_out, float& gA_out, float& gB_out) {
   static_assert(H % 32 == 0, "split MLP needs H % 32 == 0");
@@ -526,7 +562,7 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
       for (int r = 0; r < 4; ++r) {
         const int h = 16 * (T0 + t) + 4 * qq + r;
         const float acc = fmaf(ac[t][r], SPLIT_INV, am[t][r]);
-        act[0][T0 + t][r] = elu(fmaf(cm, acc, fmaf(sh.vec[H + h], tau, sh.vec[h])));
+        act[0][T0 + t][r] = Act<ACT>::f(fmaf(cm, acc, fmaf(sh.vec[H + h], tau, sh.vec[h])));
       }
   }
   // ---------------- hidden layers
@@ -543,7 +579,7 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = elu(o[t][r] + sh.bh[l * H + 16 * (T0 + t) + 4 * qq + r]);
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = Act<ACT>::f(o[t][r] + sh.bh[l * H + 16 * (T0 + t) + 4 * qq + r]);
     }
   }
   // ---------------- output u = wout . a_L + bout ; delta_L = wout * elu'(a_L)
@@ -555,7 +591,7 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
       const int h = 16 * T + 4 * qq + r;
       const float w = sh.vec[2 * H + h];
       up = fmaf(w, act[L - 1][T][r], up);
-      act[L - 1][T][r] = w * delu_from_a(act[L - 1][T][r]);
+      act[L - 1][T][r] = w * Act<ACT>::d(act[L - 1][T][r]);
     }
   u_out = qsum(up) + net.bout;
   // ---------------- backward through hidden layers: delta_l = (W_{l+1}^T delta_{l+1}) * elu'(a_l)
@@ -572,7 +608,7 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = o[t][r] * delu_from_a(act[l][T0 + t][r]);
+        for (int r = 0; r < 4; ++r) act[l][T0 + t][r] = o[t][r] * Act<ACT>::d(act[l][T0 + t][r]);
     }
   }
   // ---------------- input gradient
@@ -652,14 +688,12 @@ struct LdsGbm {
   unsigned char dl[P * DLCAP];
 };
 
-__device__ __forceinline__ float d2elu_from_a(float a) { return a > 0.f ? 0.f : a + 1.0f; }
-
 // Diagonal of the x-Hessian of u at (s, X_s) for this wave's 16 paths, contracted with the
 // path's SDGD index histogram: s1 = sum_d cnt[d] u_dd, s2 = sum_d cnt[d] |u_dd|.
 // Uses u_dd = sum_l < lam_l, elu''(z_l) * zdot_l^2 >, with lam_l = du/da_l (one backward pass)
 // and zdot_l = dz_l/dx_d (first-order tangents only): half the MACs of second-order
 // forward mode.  All GEMMs are v_mfma_f32_16x16x4_f32 in the hidden x path orientation.
-template <int H, int L>
+template <int H, int L, int ACT>
 __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt, float& s1_out,
                                           float& s2_out) {
   constexpr int HT = H / 16;
@@ -687,7 +721,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int h = 16 * T + 4 * qq + r;
-      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+      act[0][T][r] = Act<ACT>::f(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
     }
   }
 #pragma unroll
@@ -705,7 +739,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
         acc = mfma4(a.w, act[l - 1][t][3], acc);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+      for (int r = 0; r < 4; ++r) act[l][T][r] = Act<ACT>::f(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
     }
   }
   // adjoints lam_l = du/da_l
@@ -719,7 +753,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l + 1][t][r]) * lam[l + 1][t][r];
+      for (int r = 0; r < 4; ++r) Bm[t][r] = Act<ACT>::d(act[l + 1][t][r]) * lam[l + 1][t][r];
 #pragma unroll
     for (int T = 0; T < HT; ++T) {
       floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -742,7 +776,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
-        term = fmaf(lam[0][T][r] * d2elu_from_a(act[0][T][r]), z[T][r] * z[T][r], term);
+        term = fmaf(lam[0][T][r] * Act<ACT>::d2(act[0][T][r]), z[T][r] * z[T][r], term);
       }
 #pragma unroll
     for (int l = 1; l < L; ++l) {
@@ -750,7 +784,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l - 1][t][r]) * z[t][r];
+        for (int r = 0; r < 4; ++r) Bm[t][r] = Act<ACT>::d(act[l - 1][t][r]) * z[t][r];
 #pragma unroll
       for (int T = 0; T < HT; ++T) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -766,7 +800,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           z[T][r] = acc[r];
-          term = fmaf(lam[l][T][r] * d2elu_from_a(act[l][T][r]), acc[r] * acc[r], term);
+          term = fmaf(lam[l][T][r] * Act<ACT>::d2(act[l][T][r]), acc[r] * acc[r], term);
         }
       }
     }
@@ -802,7 +836,7 @@ __device__ __forceinline__ void split8u(const float (&x)[8], half8& hi, half8& l
     lo[j] = l.x, lo[j + 1] = l.y;
   }
 }
-template <int H, int L>
+template <int H, int L, int ACT>
 __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
                                                 float& s1_out, float& s2_out) {
   static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
@@ -887,10 +921,10 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int h = 16 * T + 4 * qq + r;
-      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+      act[0][T][r] = Act<ACT>::f(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
     }
   }
-  // hidden layers: B = SA a_{l-1}, o = 2^s SA W a -> a_l = elu(o wus / SA + b)
+  // hidden layers: B = SA a_{l-1}, o = 2^s SA W a -> a_l = Act<ACT>::f(o wus / SA + b)
   {
     float ones[HT][4];
 #pragma unroll
@@ -907,7 +941,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
       for (int T = 0; T < HT; ++T)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) act[l][T][r] = elu(fmaf(o[T][r], sc, sh.bh[l * H + 16 * T + 4 * qq + r]));
+        for (int r = 0; r < 4; ++r) act[l][T][r] = Act<ACT>::f(fmaf(o[T][r], sc, sh.bh[l * H + 16 * T + 4 * qq + r]));
     }
   }
   // adjoints lam_l = du/da_l: lam_l = W_{l+1}^T (elu'(a_{l+1}) lam_{l+1})  (scaled-lo WTS, once per path)
@@ -921,7 +955,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Bm[t][r] = delu_from_a(act[l + 1][t][r]) * lam[l + 1][t][r];
+      for (int r = 0; r < 4; ++r) Bm[t][r] = Act<ACT>::d(act[l + 1][t][r]) * lam[l + 1][t][r];
     half8 bh[NU], bl[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) split_act(Bm[2 * u], Bm[2 * u + 1], bh[u], bl[u]);
@@ -952,8 +986,8 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     for (int T = 0; T < HT; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        lam[l][T][r] *= d2elu_from_a(act[l][T][r]) * (zs * zs);
-        if (l < L - 1) fz[l][T][r] = delu_from_a(act[l][T][r]) * bs;
+        lam[l][T][r] *= Act<ACT>::d2(act[l][T][r]) * (zs * zs);
+        if (l < L - 1) fz[l][T][r] = Act<ACT>::d(act[l][T][r]) * bs;
       }
   }
   // tangent sweep over the state dimensions.  The lam z^2 terms accumulate in register pairs
@@ -1107,7 +1141,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 
 // u(tau, x + cmul S) for this wave's 16 paths with every weight LDS-resident (GBM layout):
 // the forward half of mlp_hdiag.  The TD terminal value (data.py:941-942).
-template <int H, int L>
+template <int H, int L, int ACT>
 __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh, int nxt) {
   constexpr int HT = H / 16;
   constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
@@ -1132,7 +1166,7 @@ __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int h = 16 * T + 4 * qq + r;
-      act[0][T][r] = elu(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
+      act[0][T][r] = Act<ACT>::f(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
     }
   }
 #pragma unroll
@@ -1150,7 +1184,7 @@ __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh,
         acc = mfma4(a.w, act[l - 1][t][3], acc);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) act[l][T][r] = elu(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
+      for (int r = 0; r < 4; ++r) act[l][T][r] = Act<ACT>::f(acc[r] + sh.bh[l * H + 16 * T + 4 * qq + r]);
     }
   }
   float up = 0.f;
@@ -1383,13 +1417,13 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     const float acc = matvec(net.W1xT, xs, nx);
     if (tid < H) {
       bx[(size_t)i * H + tid] = net.b1[tid] + acc;
-      act[0][tid] = elu(fmaf(net.w1t[tid], t, net.b1[tid] + acc));
+      act[0][tid] = act_f(net.act, fmaf(net.w1t[tid], t, net.b1[tid] + acc));
     }
     __syncthreads();
   }
   for (int l = 1; l < L; ++l) {
     const float acc = matvec(net.WT[l], act[l - 1], H);
-    if (tid < H) act[l][tid] = elu(acc + net.b[l][tid]);
+    if (tid < H) act[l][tid] = act_f(net.act, acc + net.b[l][tid]);
     __syncthreads();
   }
   if constexpr (KIND == DPI_EQ_GBM) {
@@ -1403,7 +1437,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     // adjoints: lam_l = W_{l+1}^T (elu'(a_{l+1}) * lam_{l+1}), a k-sliced mat-vec over the block with
     // every weight load in flight (W_{l+1} row-major (H_out, H_in) is its transposed operand)
     for (int l = L - 2; l >= 0; --l) {
-      if (tid < H) cb[tid] = delu_from_a(act[l + 1][tid]) * lamb[l + 1][tid];
+      if (tid < H) cb[tid] = act_d(net.act, act[l + 1][tid]) * lamb[l + 1][tid];
       __syncthreads();
       const float acc = matvec(net.W[l + 1], cb, H);
       if (tid < H) lamb[l][tid] = acc;
@@ -1420,14 +1454,14 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     for (int h = hg; h < H; h += 8) {
       const float z = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
       ztb[0][h][d] = z;
-      ud = fmaf(lamb[0][h] * d2elu_from_a(act[0][h]), z * z, ud);
+      ud = fmaf(lamb[0][h] * act_d2(net.act, act[0][h]), z * z, ud);
     }
     int cz = 0;
     const int H4 = H & ~3;
     for (int l = 1; l < L; ++l) {
       for (int q = tid; q < H * H; q += NTHB) {
         const int h = q / H, k = q - h * H;
-        wsc[h * 64 + k] = net.W[l][q] * delu_from_a(act[l - 1][k]);
+        wsc[h * 64 + k] = net.W[l][q] * act_d(net.act, act[l - 1][k]);
       }
       __syncthreads();  // wsc and Z_{l-1} complete
       float z[8];
@@ -1453,7 +1487,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
         const int h = hg + 8 * j;
         if (h < H) {
           ztb[cz ^ 1][h][d] = z[j];
-          ud = fmaf(lamb[l][h] * d2elu_from_a(act[l][h]), z[j] * z[j], ud);
+          ud = fmaf(lamb[l][h] * act_d2(net.act, act[l][h]), z[j] * z[j], ud);
         }
       }
       cz ^= 1;
@@ -1471,12 +1505,12 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   }
   const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
   int cur = 0;
-  if (tid < H) dbuf[0][tid] = net.wout[tid] * delu_from_a(act[L - 1][tid]);
+  if (tid < H) dbuf[0][tid] = net.wout[tid] * act_d(net.act, act[L - 1][tid]);
   __syncthreads();
   for (int l = L - 2; l >= 0; --l) {
     // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
     const float acc = matvec(net.W[l + 1], dbuf[cur], H);
-    if (tid < H) dbuf[cur ^ 1][tid] = acc * delu_from_a(act[l][tid]);
+    if (tid < H) dbuf[cur ^ 1][tid] = acc * act_d(net.act, act[l][tid]);
     cur ^= 1;
     __syncthreads();
   }
@@ -1554,7 +1588,7 @@ __device__ __forceinline__ void hess_accum(LdsGbm<H>& sh, const float* wgt, int 
   }
 }
 
-template <int KIND, int H, int L, bool ZERO, bool SPLIT>
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, int ACT>
 __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, const PathArgs& a, LdsGbm<H>& sh,
                                            int i, int blk, uint32_t ig, uint32_t m, float s, float smt, float tmt,
                                            float g_x, int nxp) {
@@ -1566,9 +1600,9 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
     float s1 = 0.f, s2 = 0.f;
     if constexpr (!ZERO) {
       if constexpr (SPLIT)
-        mlp_hdiag_split<H, L>(e, net, sh, nxp / 16, s1, s2);
+        mlp_hdiag_split<H, L, ACT>(e, net, sh, nxp / 16, s1, s2);
       else
-        mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+        mlp_hdiag<H, L, ACT>(e, net, sh, nxp / 16, s1, s2);
     }
     const float c1 = 0.5f * (1.0f - e.alpha), c2 = 0.25f;
     float arg[NSG], sn[NSG];
@@ -1764,7 +1798,7 @@ __device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, co
   if (threadIdx.x == 0) a.tickets[i] = 0;
 }
 
-template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false>
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
 __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
@@ -1968,9 +2002,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       float u = 0.f, gs = 0.f, gA = 0.f, gB = 0.f;
       if (!ZERO && INTG) {
         if constexpr (SPLIT)
-          mlp_tile_split<KIND, H, L>(e, net, sh, u, gs, gA, gB);
+          mlp_tile_split<KIND, H, L, ACT>(e, net, sh, u, gs, gA, gB);
         else
-          mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
+          mlp_tile<KIND, H, L, ACT>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
       }
       const int pp = 16 * wv + (lane & 15);
       if ((lane >> 4) == 0) sh.bsh[pp] = INTG ? tmt * (Eq<KIND>::ffv(e, u, gs, gA, gB) - f_b) : 0.f;
@@ -1982,9 +2016,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       if constexpr (!ZERO) {
         if (INTG) {
           if constexpr (SPLIT)
-            mlp_hdiag_split<H, L>(e, net, sh, nxp / 16, s1, s2);
+            mlp_hdiag_split<H, L, ACT>(e, net, sh, nxp / 16, s1, s2);
           else
-            mlp_hdiag<H, L>(e, net, sh, nxp / 16, s1, s2);
+            mlp_hdiag<H, L, ACT>(e, net, sh, nxp / 16, s1, s2);
         }
       }
       const float vv = (float)(e.sdgd_v > 0 ? e.sdgd_v : nx);
@@ -2055,13 +2089,13 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
     float u = 0.f;
     if constexpr (!ZERO) {
       if constexpr (GBM) {
-        u = mlp_value_res<H, L>(net, sh, nxp / 16);
+        u = mlp_value_res<H, L, ACT>(net, sh, nxp / 16);
       } else {
         float gs, gA, gB;
         if constexpr (SPLIT)
-          mlp_tile_split<KIND, H, L>(e, net, sh, u, gs, gA, gB);
+          mlp_tile_split<KIND, H, L, ACT>(e, net, sh, u, gs, gA, gB);
         else
-          mlp_tile<KIND, H, L>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
+          mlp_tile<KIND, H, L, ACT>(e, net, sh, nxp / 16, u, gs, gA, gB, nullptr, 0, P);
       }
     }
     const int pp = 16 * wv + (lane & 15);
@@ -2163,7 +2197,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
     }
   }
   if constexpr (HESS) {
-    hess_block<KIND, H, L, ZERO, SPLIT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
+    hess_block<KIND, H, L, ZERO, SPLIT, ACT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
   } else {
     if (a.tickets) fused_reduce(a, i, F, out);
   }

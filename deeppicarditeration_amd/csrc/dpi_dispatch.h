@@ -47,18 +47,20 @@ struct Launch {
 // TDV: the TD-estimator k_paths variants, compiled in translation units of their own
 // (dpi_paths_td_*.hip): sharing a unit with the plain kernels perturbs the register allocation
 // of the plain fused-MLP kernel (6 spills at 256 VGPRs instead of none at 252).
-template <int KIND, int H, int L, bool Z, bool TDV>
+// ACT: the hidden activation (DPI_ACT_*); the Tanh k_paths family lives in units of its own too
+// (dpi_paths_*_tanh.hip).  k_baseline is shape- and activation-generic (it reads net.act).
+template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if constexpr (TDV) {
     if constexpr (!Z && H % 32 == 0) {
       if (q.a->split)
-        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
                            net->d, *q.a);
       else
-        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
-                           net->d, *q.a);
+        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
+                           p->e, net->d, *q.a);
     } else {
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
                          net->d, *q.a);
     }
   } else if (q.baseline)
@@ -70,31 +72,38 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
       e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
       if constexpr (!Z && H % 32 == 0) {
         if (q.a->split) {
-          hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
-                             *q.a);
+          hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, true, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
+                             e2, net->d, *q.a);
           return;
         }
       }
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2, net->d,
-                         *q.a);
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2,
+                         net->d, *q.a);
     }
   } else if constexpr (!Z && H % 32 == 0) {
     if (q.a->split)
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+                         net->d, *q.a);
     else
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
+                         p->e, net->d, *q.a);
   } else
-    hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a);
+    hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+                       net->d, *q.a);
 }
 
-template <int KIND, bool TDV = false>
+template <int KIND, bool TDV = false, int ACT = DPI_ACT_ELU>
 bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
-  if (net->d.kind == 0) {
-    do_launch<KIND, 16, 1, true, TDV>(p, net, q);
-    return true;
+  if constexpr (ACT == DPI_ACT_ELU) {  // zero nets and the (activation-generic) baseline: the ELU units
+    if (net->d.kind == 0) {
+      do_launch<KIND, 16, 1, true, TDV>(p, net, q);
+      return true;
+    }
+  } else {
+    if (net->d.kind == 0 || q.baseline) return false;
   }
   const int H = net->d.H, L = net->d.L;
-  if constexpr (!TDV) {
+  if constexpr (!TDV && ACT == DPI_ACT_ELU) {
     if (q.baseline) {  // the baseline kernel is shape-generic
       if (KIND == DPI_EQ_GBM && H > 64) return false;
       do_launch<KIND, 16, 1, false, false>(p, net, q);
@@ -104,7 +113,7 @@ bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q)
   if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
 #define DPI_SHAPE(HH, LL)                      \
   if (H == HH && L == LL) {                    \
-    do_launch<KIND, HH, LL, false, TDV>(p, net, q); \
+    do_launch<KIND, HH, LL, false, TDV, ACT>(p, net, q); \
     return true;                               \
   }
     DPI_SHAPE(64, 3)
@@ -136,3 +145,6 @@ bool dispatch_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q)
 bool dispatch_td_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_td_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_td_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

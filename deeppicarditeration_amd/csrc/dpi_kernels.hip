@@ -291,7 +291,8 @@ static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
 }
 
 int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out) {
-  if (!out || nx < 1 || nx > NXP_MAX || !(alpha > 0)) return fail(DPI_ERR_ARG, "cha: bad arguments");
+  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "cha: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (!out || nx < 1 || !(alpha > 0)) return fail(DPI_ERR_ARG, "cha: bad arguments");
   auto* p = new_problem(DPI_EQ_CHA, nx, alpha, T);
   const double kp = k / std::sqrt((double)nx);  // equations.py:285
   const double k_alpha_d = kp * alpha * nx;
@@ -303,7 +304,8 @@ int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem
 
 int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale, int n_comp,
                           const double* mean, const double* var_diag, const double* pi, dpi_problem* out) {
-  if (!out || nx < 1 || nx > NXP_MAX || n_comp < 1 || n_comp > NSG || !mean || !var_diag || !pi)
+  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "ou: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (!out || nx < 1 || n_comp < 1 || n_comp > NSG || !mean || !var_diag || !pi)
     return fail(DPI_ERR_ARG, "ou: bad arguments (1 <= n_comp <= 8, nx <= 128)");
   auto* p = new_problem(DPI_EQ_OU, nx, alpha, T);
   p->e.ou_theta = (float)theta;
@@ -333,7 +335,8 @@ int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double m
 
 int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
                            dpi_problem* out) {
-  if (!out || nx < 1 || nx > NXP_MAX || n_nodes < 1 || n_nodes > NSG || !w || !v)
+  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "gbm: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (!out || nx < 1 || n_nodes < 1 || n_nodes > NSG || !w || !v)
     return fail(DPI_ERR_ARG, "gbm: bad arguments (1 <= n_nodes <= 8, nx <= 128)");
   auto* p = new_problem(DPI_EQ_GBM, nx, alpha, T);
   p->e.nodes = n_nodes;
@@ -449,16 +452,52 @@ int dpi_net_status_peek(dpi_net net, int slot, int* status) {
 
 int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params, size_t n_params,
                        dpi_net* out) {
-  if (!out || !widths || !params || n_in < 2 || n_in - 1 > NXP_MAX || n_hidden < 1 || n_hidden > 4)
+  if (n_in - 1 > NXP_MAX)
+    return fail(DPI_ERR_UNSUPPORTED, "mlp: nx = n_in - 1 exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (!out || !widths || !params || n_in < 2 || n_hidden < 1 || n_hidden > 4)
     return fail(DPI_ERR_ARG, "mlp: bad arguments");
-  if (act != DPI_ACT_ELU) return fail(DPI_ERR_UNSUPPORTED, "mlp: only ELU activations are supported");
-  const int H = widths[0];
-  for (int l = 1; l < n_hidden; ++l)
-    if (widths[l] != H) return fail(DPI_ERR_UNSUPPORTED, "mlp: hidden widths must be equal");
-  if (!(H == 16 || H == 32 || H == 64 || H == 128)) return fail(DPI_ERR_UNSUPPORTED, "mlp: width must be 16/32/64/128");
-  const int nx = n_in - 1, nxp = (nx + 15) & ~15, L = n_hidden;
-  const size_t expect = (size_t)H * n_in + H + (size_t)(L - 1) * (H * H + H) + H + 1;
+  if (act != DPI_ACT_ELU && act != DPI_ACT_TANH)
+    return fail(DPI_ERR_UNSUPPORTED, "mlp: activations must be DPI_ACT_ELU or DPI_ACT_TANH");
+  // Any hidden widths up to 128: the layers are zero-padded to the smallest compiled width H in
+  // {16, 32, 64, 128} that holds the widest one.  A padded unit has zero weights and bias in and
+  // zero weights out, so its activation (ELU(0) = tanh(0) = 0) and every gradient through it add
+  // exact zeros: the labels are those of the unpadded network.
+  int wmax = 0;
+  size_t expect = 0;
+  for (int l = 0; l < n_hidden; ++l) {
+    if (widths[l] < 1 || widths[l] > HMAX) return fail(DPI_ERR_UNSUPPORTED, "mlp: hidden widths must be in [1, 128]");
+    wmax = std::max(wmax, widths[l]);
+    expect += (size_t)widths[l] * ((l ? widths[l - 1] : n_in) + 1);
+  }
+  expect += (size_t)widths[n_hidden - 1] + 1;
   if (n_params != expect) return fail(DPI_ERR_ARG, "mlp: parameter count mismatch");
+  const float* const given = params;  // the finiteness scan (range guard) reads the caller's values
+  const int H = wmax <= 16 ? 16 : wmax <= 32 ? 32 : wmax <= 64 ? 64 : 128;
+  const int nx = n_in - 1, nxp = (nx + 15) & ~15, L = n_hidden;
+  std::vector<float> padded;
+  bool same = true;
+  for (int l = 0; l < n_hidden; ++l) same = same && widths[l] == H;
+  if (!same) {  // re-lay the parameters out as the equal-width-H network
+    padded.assign((size_t)H * n_in + H + (size_t)(L - 1) * (H * H + H) + H + 1, 0.f);
+    const float* src = params;
+    float* dst = padded.data();
+    int win = n_in, wpad_in = n_in;
+    for (int l = 0; l < L; ++l) {
+      const int w = widths[l];
+      for (int r = 0; r < w; ++r)
+        for (int c = 0; c < win; ++c) dst[(size_t)r * wpad_in + c] = src[(size_t)r * win + c];
+      src += (size_t)w * win;
+      dst += (size_t)H * wpad_in;
+      for (int r = 0; r < w; ++r) dst[r] = src[r];
+      src += w;
+      dst += H;
+      win = w;
+      wpad_in = H;
+    }
+    for (int c = 0; c < win; ++c) dst[c] = src[c];
+    dst[H] = src[win];
+    params = padded.data();
+  }
   // host-side repack
   std::vector<float> blob;
   auto take = [&](size_t cnt) {
@@ -534,6 +573,7 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   n->d.H = H;
   n->d.L = L;
   n->d.nxp = nxp;
+  n->d.act = act;
   n->d.W1x = base + oW1x;
   n->d.w1t = base + ow1t;
   n->d.b1 = base + ob1;
@@ -558,7 +598,7 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
       n->d.wus[l] = wus[l];
     }
   }
-  if (int rc = net_init_status(n, params, n_params)) {
+  if (int rc = net_init_status(n, given, n_params)) {
     dpi_net_destroy(n);
     return rc;
   }
@@ -568,7 +608,9 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
 
 int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, const float* params, size_t n_params,
                            dpi_net* out) {
-  if (!out || !hidden || !params || nx < 1 || nx > NXP_MAX || n_hidden < 1 || n_hidden > 4)
+  if (nx > NXP_MAX)
+    return fail(DPI_ERR_UNSUPPORTED, "pisgrad: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (!out || !hidden || !params || nx < 1 || n_hidden < 1 || n_hidden > 4)
     return fail(DPI_ERR_ARG, "pisgrad: bad arguments (1 <= n_hidden <= 4, nx <= 128)");
   for (int l = 0; l < n_hidden; ++l)
     if (hidden[l] < 4 || hidden[l] > 1024 || (hidden[l] % 4)) return fail(DPI_ERR_ARG, "pisgrad: hidden widths % 4");
@@ -1191,6 +1233,18 @@ extern "C" int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t
 
 static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   const bool td = q.td && !q.baseline && !q.hess;
+  if (net->d.kind == 1 && net->d.act == DPI_ACT_TANH && !q.baseline) {  // the Tanh k_paths units
+    switch (p->e.kind) {
+      case DPI_EQ_CHA:
+        return dispatch_cha_tanh(p, net, q);
+      case DPI_EQ_OU:
+        return dispatch_ou_tanh(p, net, q);
+      case DPI_EQ_GBM:
+        return dispatch_gbm_tanh(p, net, q);
+      default:
+        return false;
+    }
+  }
   switch (p->e.kind) {
     case DPI_EQ_CHA:
       return td ? dispatch_td_cha(p, net, q) : dispatch_cha(p, net, q);

@@ -80,8 +80,9 @@ class ShardedLabeler:
         if self.world == 1:
             return flag
         import torch.distributed as dist
-        dev = "cpu" if dist.get_backend(self.group) == "gloo" else self.gen.device
-        t = torch.tensor([float(flag)], device=dev)
+        # a device tensor under RCCL and under gloo alike (gloo stages it through the host), so the
+        # one-GPU gloo rehearsal runs the RCCL branch's code
+        t = torch.tensor([float(flag)], device=getattr(self.gen, "device", "cpu"))
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 

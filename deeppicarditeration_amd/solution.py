@@ -151,8 +151,12 @@ class DeviceNet:
         if isinstance(m, torch.nn.Sequential):
             lin = [l for l in m if isinstance(l, torch.nn.Linear)]
             acts = [type(l).__name__ for l in m if not isinstance(l, torch.nn.Linear)]
-            if any(a != "ELU" for a in acts):
-                raise NotImplementedError(f"MLP activations {acts}: only ELU is compiled into the label kernels")
+            # construct_mlp's activations (picard/solution.py:123-135): the label kernels are compiled
+            # for ELU (alpha = 1) and Tanh, the same one in every hidden layer
+            act_code = {"ELU": _lib.DPI_ACT_ELU, "Tanh": _lib.DPI_ACT_TANH}.get(acts[0] if acts else "ELU")
+            if act_code is None or any(a != acts[0] for a in acts):
+                raise NotImplementedError(f"MLP activations {acts}: the label kernels are compiled for all-ELU or "
+                                          "all-Tanh hidden layers")
             if any(l.alpha != 1.0 for l in m if isinstance(l, torch.nn.ELU)):
                 raise NotImplementedError("ELU alpha != 1")
             if lin[-1].out_features != 1:
@@ -164,10 +168,10 @@ class DeviceNet:
                                                    l.bias.detach().cpu().double().numpy().ravel()]) for l in lin])
             flat = np.ascontiguousarray(flat, np.float32)
             w = (_lib.c_int * len(widths))(*widths)
-            _lib.check(lib.dpi_net_create_mlp(n_in, len(widths), w, _lib.DPI_ACT_ELU,
+            _lib.check(lib.dpi_net_create_mlp(n_in, len(widths), w, act_code,
                                               flat.ctypes.data_as(_lib.P(_lib.c_float)), flat.size, h),
                        "dpi_net_create_mlp")
-            return cls(h, f"mlp{widths}")
+            return cls(h, f"mlp{widths}" + ("" if act_code == _lib.DPI_ACT_ELU else "-tanh"))
         if isinstance(m, PISGradNet) or type(m).__name__ == "PISGradNet":
             return cls._from_pisgrad(lib, m, n_in)
         raise NotImplementedError(f"network type {type(m).__name__} has no device implementation in this build")

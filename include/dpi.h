@@ -69,6 +69,7 @@ extern "C" {
 
 /* activations */
 #define DPI_ACT_ELU 1
+#define DPI_ACT_TANH 2
 
 /* estimator selection (dpi_label_moments / finalize flags) */
 #define DPI_TERMINAL 1 /* estimate_terminal_with_gradients (data.py:899-926) */
@@ -89,7 +90,10 @@ int dpi_abi_version(void);
 /* Copies the calling thread's last error message (NUL-terminated); returns its length. */
 int dpi_last_error(char* buf, size_t len);
 
-/* --- problem plugins (host parameters copied to device; fp64 in, fp32 on device) --- */
+/* --- problem plugins (host parameters copied to device; fp64 in, fp32 on device) ---
+ * The state dimension is compiled up to nx = 128 (NXP_MAX: the path kernels' LDS noise tile, the
+ * fused MLP's input chunks and k_pis_net's X image are sized for it); a larger nx fails with
+ * DPI_ERR_UNSUPPORTED naming the cap (the reference's shipped configurations are 10-d and 100-d). */
 int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out);
 /* mean: (n_comp, nx); var_diag: (n_comp, nx) diagonal of each component covariance; pi: (n_comp) */
 int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale,
@@ -117,7 +121,9 @@ int dpi_net_create_zero(dpi_net* out);
 /* params: host fp32, torch state-dict order of construct_mlp(n_in, 1, widths, act):
  *   W0 (widths[0] x n_in), b0, W1 (widths[1] x widths[0]), b1, ..., Wout (1 x widths[-1]), bout.
  * Supported (width, n_hidden): all hidden widths equal, one of 16/32/64/128, n_hidden 1..4
- * (GBM: width <= 64). */
+ * (GBM: width <= 64).  act: the activation of every hidden layer, DPI_ACT_ELU (torch.nn.ELU,
+ * alpha = 1) or DPI_ACT_TANH (torch.nn.Tanh, the reference's default NETWORK.ACTIVATIONS,
+ * picard/config.py:61). */
 int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params,
                        size_t n_params, dpi_net* out);
 /* PISGradNet(hidden_shapes, dim = nx, g0 = equation.g, T) for OUProcessEquation; params: host fp32 in

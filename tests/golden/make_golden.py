@@ -162,7 +162,8 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
     if zero:
         net = sols.ZeroSolution(1)
     elif net_kind == "mlp":
-        net = sols.construct_mlp(1 + eq.nx, 1, net_kw["neurons"], ["ELU"] * len(net_kw["neurons"]), None)
+        net = sols.construct_mlp(1 + eq.nx, 1, net_kw["neurons"],
+                                 [net_kw.get("act", "ELU")] * len(net_kw["neurons"]), None)
     else:
         net = sols.PISGradNet(hidden_shapes=net_kw["neurons"], dim=eq.nx, g0=eq.g, T=eq.T)
     if weight_scale != 1.0:
@@ -198,6 +199,8 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
         for k, val in state_dict_np(net).items():
             out[f"sd_{k}"] = val
         out["neurons"] = np.asarray(net_kw["neurons"])
+        if net_kind == "mlp":
+            out["acts"] = np.asarray([net_kw.get("act", "ELU")] * len(net_kw["neurons"]))
     if eq_name == "OUProcessEquation":
         out["gmm_mean"] = eq.mean.numpy()
         out["gmm_var"] = torch.diagonal(eq.var, dim1=1, dim2=2).numpy()
@@ -273,6 +276,20 @@ def main(only=None):
              workdir=wd, picard_N=3, picard_i=3, t_uniform=False)
     run_case("tprod_gbm_mlp16_sdgd_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 5, 64, 1, 33,
              v=100, workdir=wd, picard_N=9, picard_i=3, t_uniform=False)
+    # torch.nn.Tanh hidden layers (the reference's default NETWORK.ACTIVATIONS, picard/config.py:61)
+    run_case("cha_mlp16_tanh_K2", "Cha", cha, "mlp", {"neurons": [16, 16], "act": "Tanh"}, 4, 64, 2, 51, workdir=wd)
+    run_case("cha_mlp128x4_tanh_K3", "Cha", cha, "mlp", {"neurons": [128] * 4, "act": "Tanh"}, 2, 64, 3, 52,
+             epoch=1, workdir=wd)
+    run_case("ou_mlp64x2_tanh_K2", "OUProcessEquation", ou, "mlp", {"neurons": [64, 64], "act": "Tanh"}, 3, 64, 2,
+             53, workdir=wd)
+    run_case("gbm_mlp64x3_tanh_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [64] * 3, "act": "Tanh"},
+             2, 64, 2, 54, v=100, workdir=wd)
+    run_case("gbm_mlp16_tanh_full_K1", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16], "act": "Tanh"},
+             2, 64, 1, 55, workdir=wd)
+    run_case("gbm_hess_mlp32x3_tanh_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [32] * 3, "act": "Tanh"},
+             2, 64, 2, 56, workdir=wd, hessians=True)
+    run_case("td_cha_mlp32_tanh_K2", "Cha", cha, "mlp", {"neurons": [32, 32], "act": "Tanh"}, 6, 64, 2, 57,
+             workdir=wd, delta_t=0.35)
     shutil.rmtree(wd)
 
 

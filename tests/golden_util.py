@@ -47,6 +47,11 @@ def oracle_equation(f):
     raise ValueError(eq)
 
 
+def acts(f, n_hidden):
+    """The hidden activations of an MLP fixture (ELU unless the fixture names them)."""
+    return [str(a) for a in f["acts"]] if "acts" in f else ["ELU"] * n_hidden
+
+
 def state_dict(f):
     return {k[3:]: f[k] for k in f if k.startswith("sd_")}
 
@@ -60,5 +65,5 @@ def oracle_net(f, eq):
         idx = sorted({int(k.split(".")[0]) for k in sd})
         Ws = [sd[f"{i}.weight"] for i in idx]
         bs = [sd[f"{i}.bias"] for i in idx]
-        return O.MLP(Ws, bs, ["ELU"] * (len(Ws) - 1))
+        return O.MLP(Ws, bs, acts(f, len(Ws) - 1))
     return O.PISGradNet(sd, eq, T=eq.T)

@@ -3,7 +3,7 @@ import numpy as np
 import torch
 
 import deeppicarditeration_amd as dpi
-from golden_util import delta_t, state_dict, t_factors
+from golden_util import acts, delta_t, state_dict, t_factors
 
 
 def product_equation(f):
@@ -28,7 +28,7 @@ def product_module(f, eq):
     sd = {k: torch.as_tensor(v).float() for k, v in state_dict(f).items()}
     if kind == "mlp":
         neurons = [int(v) for v in f["neurons"]]
-        m = dpi.construct_mlp(1 + eq.nx, 1, neurons, ["ELU"] * len(neurons), None)
+        m = dpi.construct_mlp(1 + eq.nx, 1, neurons, acts(f, len(neurons)), None)
         m.load_state_dict(sd)
         return m
     m = dpi.PISGradNet(hidden_shapes=[int(v) for v in f["neurons"]], dim=eq.nx, g0=eq.g, T=eq.T)

@@ -44,6 +44,15 @@ def test_host_side_argument_errors_without_gpu():
     h = ctypes.c_void_p()
     assert lib.dpi_problem_create_cha(0, 1.0, 5.0, 1.0, h) == _lib.DPI_ERR_ARG
     assert "cha" in _lib.last_error()
+    # the compiled state-dimension cap is a named refusal (include/dpi.h)
+    assert lib.dpi_problem_create_cha(200, 1.0, 5.0, 1.0, h) == _lib.DPI_ERR_UNSUPPORTED
+    assert "128" in _lib.last_error()
+    assert lib.dpi_net_create_mlp(201, 2, (ctypes.c_int * 2)(16, 16), _lib.DPI_ACT_ELU,
+                                  (ctypes.c_float * 1)(), 1, ctypes.byref(ctypes.c_void_p())) == _lib.DPI_ERR_UNSUPPORTED
+    assert "128" in _lib.last_error()
+    # activations: ELU and Tanh only
+    assert lib.dpi_net_create_mlp(101, 2, (ctypes.c_int * 2)(16, 16), 3, (ctypes.c_float * 1)(), 1,
+                                  ctypes.byref(ctypes.c_void_p())) == _lib.DPI_ERR_UNSUPPORTED
     assert lib.dpi_problem_create_cha(100, 1.0, 5.0, 1.0, h) == 0
     n = ctypes.c_void_p()
     assert lib.dpi_net_create_zero(n) == 0

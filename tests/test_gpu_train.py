@@ -287,3 +287,20 @@ def test_picard_train_burgers_shipped_sizes_iteration1_known_answer(tmp_path):
     runner.i = 0
     hist = runner.run()
     assert len(hist) == 1 and hist[0]["labels"] == 4096 and hist[0]["path_labels_per_s"] > 1e7
+
+
+def test_picard_train_with_the_default_tanh_activations(tmp_path):
+    """A YAML that leaves NETWORK.ACTIVATIONS (and NEURONS) to the defaults — the reference's
+    ["Tanh", "Tanh"] over [10, 10] (picard/config.py:60-61) — runs on the device path: Tanh
+    kernels, widths zero-padded to the compiled 16."""
+    yaml = CHA.replace("  NEURONS: [32, 32]\n  ACTIVATIONS: [ELU, ELU]\n", "").replace("PICARD: {{N: 3}}", "PICARD: {{N: 2}}")
+    assert "ACTIVATIONS" not in yaml and "NEURONS" not in yaml
+    f = tmp_path / "cha_tanh.yaml"
+    f.write_text(yaml.format(name=tmp_path / "run_tanh"))
+    runner = PicardRunner(load_cfg(str(f)))
+    assert list(runner.cfg.NETWORK.ACTIVATIONS) == ["Tanh", "Tanh"]
+    hist = runner.run()
+    assert [h["iter"] for h in hist] == [1, 2]
+    net = runner.u_current
+    assert isinstance(net[1], torch.nn.Tanh) and net[0].out_features == 10
+    assert all(h["rel_l2_u"] is not None and h["rel_l2_u"] == h["rel_l2_u"] for h in hist)

@@ -20,7 +20,7 @@ import pytest
 
 from deeppicarditeration_amd.build import build, kernel_resources
 
-ALLOWED_SPILL = {"void dpi::k_paths<2, 128, 4, false, false, false, false>(dpi::EqDev, dpi::NetDev, dpi::PathArgs)"}
+ALLOWED_SPILL = {"void dpi::k_paths<2, 128, 4, false, false, false, false, 1>(dpi::EqDev, dpi::NetDev, dpi::PathArgs)"}
 
 CEILINGS = {"dpi::k_pis_net<": 232, "dpi::k_pis_rollout_shared<": 48, "dpi::k_pis_rollout<": 64,
             "dpi::k_gemm_x3h<": 224}
