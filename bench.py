@@ -79,7 +79,7 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--prewarm-s", type=float, default=0.3, help="untimed steps for this long before the warmup")
@@ -92,11 +92,12 @@ def parse():
                                                            "baseline on a low-priority side stream, the path "
                                                            "kernels on a high-priority stream")
     ap.add_argument("--no-prepare", action="store_true", help="one stream (overrides --prepare and the hjb default)")
-    ap.add_argument("--range-check", choices=("step", "region", "off"), default="step",
-                    help="the product's range guard (data.RangeGroup) inside the timed region: 'step' (default) = "
-                         "one group per step, verified one step behind as the dataset surface does per label "
-                         "buffer; 'region' = one group over the timed steps, as picard train's LabelBuffer.fill; "
-                         "'off' = unguarded (finiteness asserted afterwards)")
+    ap.add_argument("--range-check", choices=("step", "region", "off"), default="region",
+                    help="the product's range guard (data.RangeGroup) inside the timed region: 'region' (default) = "
+                         "one group over the timed steps, verified before the clock stops, as picard train's "
+                         "LabelBuffer.fill checks one Picard iteration's labels; 'step' = one group per step, "
+                         "verified one step behind, as the dataset surface checks each label buffer; 'off' = "
+                         "unguarded (finiteness asserted afterwards)")
     ap.add_argument("--no-fp32-pass", action="store_true", help="skip the untimed exact-fp32 comparison pass")
     return ap.parse_args()
 

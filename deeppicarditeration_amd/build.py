@@ -51,6 +51,19 @@ def needs_build():
     return BUILD_ID_FILE.read_text().strip() != source_hash()
 
 
+def includes(path, seen=None):
+    """`path` and every file it #includes with quotes, transitively (the object's dependencies)."""
+    import re
+    seen = set() if seen is None else seen
+    path = Path(path).resolve()
+    if path in seen or not path.exists():
+        return seen
+    seen.add(path)
+    for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', path.read_text(), flags=re.M):
+        includes(path.parent / inc, seen)
+    return seen
+
+
 def build(force=False, verbose=True):
     if not force and not needs_build():
         return OUT
@@ -64,12 +77,10 @@ def build(force=False, verbose=True):
         subprocess.run(cmd, check=True)
         return obj
 
-    headers = sorted(CSRC.glob("*.h")) + [REPO / "include" / "dpi.h"]
-    newest_header = max(h.stat().st_mtime for h in headers)
-
-    def stale(u):  # an object is rebuilt when its unit or any shared header is newer
+    def stale(u):  # an object is rebuilt when its unit or a header it includes (transitively) is newer
         obj = OBJ / (Path(u).stem + ".o")
-        return force or not obj.exists() or obj.stat().st_mtime < max(newest_header, (CSRC / u).stat().st_mtime)
+        newest = max(f.stat().st_mtime for f in includes(CSRC / u))
+        return force or not obj.exists() or obj.stat().st_mtime < newest
 
     bid = source_hash()  # before compiling: a source edited during the build leaves the result stale
     todo = [u for u in UNITS if stale(u)]

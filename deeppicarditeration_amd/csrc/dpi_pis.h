@@ -268,6 +268,9 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
                                                            int stage, float td_dt,
                                                            int bx0, int ntask, int* __restrict__ queue,
                                                            int* __restrict__ claim, int waves) {
+#ifdef DPI_PIS_SHARED_PRIO  // measurement knob: the rollout wave's issue priority (k_pis_net runs at 2)
+  __builtin_amdgcn_s_setprio(DPI_PIS_SHARED_PRIO);
+#endif
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);         // HW_REG_HW_ID
   const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // HW_REG_XCC_ID
   const unsigned slot = (xcc << 10) | (((hw >> 8) & 0xffu) << 2) | ((hw >> 4) & 3u);

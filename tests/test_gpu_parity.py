@@ -376,8 +376,8 @@ def test_unsupported_configurations_fail_loudly():
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd._lib import DPIError
     eq = dpi.Cha(100, 1.0, 5.0, 1.0)
-    with pytest.raises(NotImplementedError):
-        dpi.OnlineDataGenerator(eq, dpi.construct_mlp(101, 1, [16], ["Tanh"], None), 1, 1, device="cuda:0",
+    with pytest.raises(NotImplementedError):  # activations other than ELU / Tanh (tests/test_gpu_tanh.py)
+        dpi.OnlineDataGenerator(eq, dpi.construct_mlp(101, 1, [16], ["Softplus"], None), 1, 1, device="cuda:0",
                                 t_always_uniform=True, n_estimate_terminal=64, n_estimate_integral=64)
     with pytest.raises(ValueError):
         dpi.OnlineDataGenerator(eq, dpi.ZeroSolution(), 1, 1, device="cuda:0", t_always_uniform=True,

@@ -113,7 +113,7 @@ def test_uncompiled_widths_are_zero_padded(widths, act, mode):
     gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
                                   n_estimate_integral=128, n_euler_steps=4, seed=5)
     tx, y = gen.sample_with_gradients(3)
-    ref = O.labels_grad(oeq, _oracle_mlp(net, [act] * len(widths)), tx.cpu().double().numpy(), 128, 4, 5, 0, 0)
+    ref = O.labels_grad(oeq, _oracle_mlp(net, [act] * len(widths)), tx.cpu().double().numpy(), 128, 4, 5, 1, 0)
     p = _parts(y.cpu().numpy(), ref)
     assert max(p.values()) < TOL, p
 
