@@ -1555,7 +1555,71 @@ struct PathArgs {
   int* rd_status;
   float rd_invM, rd_bound;
   int rd_add_g;
+  // GBM prepared calls (dpi_label_prepare): the noise sums of phase 1, already rolled out by
+  // k_noise_shared beside the previous batch's path launch, [n][nbp][2 (terminal, integral)][4 nb][P]
+  const float* noise;
 };
+
+// Noise sums of a (point, block, estimator part, wave slice) task: exactly the K-step loops of
+// k_paths' terminal / integral rollouts (same counters, same sequential sum per dimension, the same
+// BM_SCALE product), so a path launch that reads them is bitwise the one that rolls out itself.
+template <int UNR>
+__device__ __forceinline__ void noise_task(const PathArgs& a, int nb, int t) {
+  const int lane = threadIdx.x & 63;
+  const int blkg = t >> 3, part = (t >> 2) & 1, wq = t & 3;  // 8 tasks per (point, block)
+  const int i = blkg / a.nbp, blk = blkg - i * a.nbp;
+  const uint32_t ig = a.point_base + (uint32_t)i;
+  const uint32_t m = (uint32_t)(a.m_begin + P * blk + lane);
+  const uint32_t c3 = part ? a.c3i : a.c3t;
+  float* out = const_cast<float*>(a.noise) + ((size_t)blkg * 2 + part) * (4 * nb) * P + lane;
+  if (!(a.flags & (part ? DPI_INTEGRAL : DPI_TERMINAL))) return;
+  for (int j = wq; j < nb; j += 4) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll UNR
+    for (int k = 0; k < a.K; ++k) {
+      const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3, a.k0, a.k1));
+      s0 += z.a;
+      s1 += z.b;
+      s2 += z.c;
+      s3 += z.d;
+    }
+    out[(4 * j + 0) * P] = s0 * BM_SCALE;
+    out[(4 * j + 1) * P] = s1 * BM_SCALE;
+    out[(4 * j + 2) * P] = s2 * BM_SCALE;
+    out[(4 * j + 3) * P] = s3 * BM_SCALE;
+  }
+}
+
+// The prepare stream's noise pre-pass for the GBM path launch (dpi_label_prepare): a work queue of
+// the 8 n nbp one-wave tasks served by at most `waves` waves per SIMD, the pattern of
+// k_pis_rollout_shared: the first waves of the launch on a SIMD claim it (per-SIMD word keyed by
+// HW_ID and XCC_ID, zeroed with the queue counter before the launch) and take tasks until the queue
+// is empty, every other wave leaves at once.  <= 48 registers and no LDS, so one such wave fits on
+// each SIMD beside a k_paths<GBM> wave (<= 464 registers, 162 KB of LDS per CU) of the previous
+// batch and issues VALU work in the slots its tangent sweep leaves idle.  Every wave reaches the
+// exit: a claimed wave ends when the queue counter passes ntask.
+#ifndef DPI_NOISE_SHARED_UNR
+#define DPI_NOISE_SHARED_UNR 4
+#endif
+template <int UNR>
+__global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(24))) void k_noise_shared(PathArgs a, int nb,
+                                                                                         int ntask, int* queue,
+                                                                                         int* claim, int waves) {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);         // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+  const unsigned slot = (xcc << 10) | (((hw >> 8) & 0xffu) << 2) | ((hw >> 4) & 3u);
+  const int lane = threadIdx.x & 63;
+  int old = 0;
+  if (lane == 0) old = atomicAdd(claim + slot, 1);
+  if (__builtin_amdgcn_readfirstlane(old) >= waves) return;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = atomicAdd(queue, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= ntask) break;
+    noise_task<UNR>(a, nb, t);
+  }
+}
 
 // ------------------------------------------------------------------------------ Hessian labels
 // Malliavin-weight Hessian block of generate_with_gradients_and_hessians (picard/data.py:1220-1223;
@@ -1832,6 +1896,8 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   const float g_x = a.gx[i], f_b = a.fb[i];
   const float Kf = (float)a.K;
   constexpr bool STAMP = GBM && !ZERO && !HESS && !TD;
+  // GBM prepared calls: phase 1's noise sums come from k_noise_shared (a wave-uniform branch)
+  const bool PRE = GBM && !HESS && !TD && a.noise != nullptr;
   DPI_STAMP(STAMP, 0);
 
   for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
@@ -1923,19 +1989,25 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       const int j = wv + 4 * c;  // terminal dim-blocks of this wave
       ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
       if (TERM && j < nb) {
-        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        #pragma unroll NOISE_UNROLL
-        for (int k = 0; k < a.K; ++k) {
-          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
-          s0 += z.a;
-          s1 += z.b;
-          s2 += z.c;
-          s3 += z.d;
+        if (PRE) {  // rolled out by k_noise_shared (GBM prepared calls)
+          const float* np = a.noise + ((size_t)(i * a.nbp + blk) * 2) * (4 * nb) * P + lane;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ST[c][q] = np[(4 * j + q) * P];
+        } else {
+          float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+          #pragma unroll NOISE_UNROLL
+          for (int k = 0; k < a.K; ++k) {
+            const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
+            s0 += z.a;
+            s1 += z.b;
+            s2 += z.c;
+            s3 += z.d;
+          }
+          ST[c][0] = s0 * BM_SCALE;
+          ST[c][1] = s1 * BM_SCALE;
+          ST[c][2] = s2 * BM_SCALE;
+          ST[c][3] = s3 * BM_SCALE;
         }
-        ST[c][0] = s0 * BM_SCALE;
-        ST[c][1] = s1 * BM_SCALE;
-        ST[c][2] = s2 * BM_SCALE;
-        ST[c][3] = s3 * BM_SCALE;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int d = 4 * j + q;
@@ -1950,7 +2022,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
       const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
       if (j < nb) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        if (INTG) {
+        if (INTG && !PRE) {
           #pragma unroll NOISE_UNROLL
           for (int k = 0; k < a.K; ++k) {
             const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
@@ -1960,7 +2032,12 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
             s3 += z.d;
           }
         }
-        const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+        float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
+        if (INTG && PRE) {  // rolled out by k_noise_shared (GBM prepared calls)
+          const float* np = a.noise + ((size_t)(i * a.nbp + blk) * 2 + 1) * (4 * nb) * P + lane;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) sv[q] = np[(4 * j + q) * P];
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int d = 4 * j + q;

@@ -910,11 +910,21 @@ static int pis_chunk_wg() {
 
 // Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | [PIS rows] | partial[n][2F][nbp]  (256-B aligned)
 struct WsLayout {
-  size_t gx, fb, bx, hb, tk, rows, partial, rq, total;
+  size_t gx, fb, bx, hb, tk, rows, partial, rq, noise, nq, total;
   int rows_cap;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
-static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
+// GBM MLP nets stage their noise sums on the prepare stream (dpi_label_prepare -> k_noise_shared;
+// DPI_GBM_PREP=0 disables it): the workspace then holds them, [n][nbp][2][4 nb][P] floats.
+static bool gbm_noise_prep(dpi_problem p, dpi_net net) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("DPI_GBM_PREP");
+    v = (!e || std::atoi(e) != 0) ? 1 : 0;
+  }
+  return v && p && net && net->d.kind == 1 && p->e.kind == DPI_EQ_GBM;
+}
+static WsLayout ws_layout(dpi_net net, int n, int M, int F, bool noise = false) {
   WsLayout w;
   const int H = (net && net->d.kind == 1) ? net->d.H : 0;
   const size_t nbp = (size_t)(M + P - 1) / P;
@@ -935,7 +945,11 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F) {
   w.partial = w.rows + rows_bytes;
   w.rq = w.partial + al256((size_t)n * nbp * slab_row(F) * 4);
   // PISGradNet: the shared rollout's queue counter (256 B) and per-SIMD claim words
-  w.total = w.rq + ((net && net->d.kind == 2) ? 256 + (size_t)PIS_CLAIM_SLOTS * 4 : 0);
+  w.noise = w.rq + ((net && net->d.kind == 2) ? 256 + (size_t)PIS_CLAIM_SLOTS * 4 : 0);
+  const size_t nb4 = (size_t)((F - 1 + 3) / 4) * 4;
+  w.nq = w.noise + (noise ? al256((size_t)n * nbp * 2 * nb4 * P * 4) : 0);
+  // k_noise_shared's queue counter (256 B) and per-SIMD claim words
+  w.total = w.nq + (noise ? 256 + (size_t)PIS_CLAIM_SLOTS * 4 : 0);
   return w;
 }
 
@@ -1179,7 +1193,7 @@ static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st
 
 extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) {
   if (!p || n < 0 || M < 0) return 0;
-  return ws_layout(net, n, M, 1 + p->e.nx).total;
+  return ws_layout(net, n, M, 1 + p->e.nx, gbm_noise_prep(p, net)).total;
 }
 
 // the counters of draws 1-3 (k_sample_points, k_baseline's in-block sampling)
@@ -1482,7 +1496,7 @@ static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   const int F = 1 + p->e.nx;
   const int nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "label_moments: at most DPI_PATHS_PER_CALL_MAX paths per call");
-  *w = ws_layout(net, n, M, F);
+  *w = ws_layout(net, n, M, F, gbm_noise_prep(p, net));
   if (ws_bytes < w->total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
   char* b = (char*)ws;
   PathArgs& a = *pa;
@@ -1511,6 +1525,7 @@ static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   return 0;
 }
 
+static bool stages_prepare(dpi_problem p, dpi_net net);
 static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                         uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                         void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
@@ -1528,6 +1543,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
+    if ((flags & DPI_PREPARED) && stages_prepare(p, net)) a.noise = (const float*)(b + w.noise);
     if (nbp <= 64 && fused_reduce_on()) {  // k_paths' last block per point reduces and finalizes
       if (!base_tag_ok(ws, n))
         return fail(DPI_ERR_ARG, "label_moments: no dpi_point_baseline / dpi_sample_points_baseline of these n points "
@@ -1641,7 +1657,9 @@ static void prep_tags_drop(const void* owner) {
     it = (it->second.p == owner || it->second.net == owner) ? prep_tags().erase(it) : std::next(it);
 }
 
-static bool stages_prepare(dpi_problem p, dpi_net net) { return net->d.kind == 2 && !(p->td_dt > 0.f); }
+static bool stages_prepare(dpi_problem p, dpi_net net) {
+  return (net->d.kind == 2 || gbm_noise_prep(p, net)) && !(p->td_dt > 0.f);
+}
 
 int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed, uint32_t epoch,
                       uint32_t point_base, int m_begin, int m_end, int flags, void* ws, size_t ws_bytes, void* stream) {
@@ -1655,6 +1673,18 @@ int dpi_label_prepare(dpi_problem p, dpi_net net, const float* tx, int n, int M,
     std::lock_guard<std::mutex> g(g_prep_mu);
     prep_tags()[ws] =
         PrepTag{p, net, tx, n, M, K, m_begin, m_end, flags & DPI_BOTH, pis_x3(net) ? 1 : 0, seed, epoch, point_base, ws_bytes};
+  }
+  if (net->d.kind == 1) {  // GBM: phase 1's noise sums, one wave per SIMD beside the previous path launch
+    char* b = (char*)ws;
+    hipStream_t st = (hipStream_t)stream;
+    int* nq = (int*)(b + w.nq);
+    HIPCHK(hipMemsetAsync(nq, 0, 256 + (size_t)PIS_CLAIM_SLOTS * 4, st));
+    a.noise = (const float*)(b + w.noise);
+    const int nb = (p->e.nx + 3) / 4;
+    hipLaunchKernelGGL(k_noise_shared<DPI_NOISE_SHARED_UNR>, dim3(4 * cu_count() * 3), dim3(P), 0, st, a, nb,
+                       n * a.nbp * 8, nq, nq + 64, 1);
+    HIPCHK(hipGetLastError());
+    return 0;
   }
   return pis_paths(p, net, tx, n, K, a, w, (char*)ws, (hipStream_t)stream, false, true);
 }

@@ -413,14 +413,17 @@ class OnlineDataGenerator:
             on_moments_end()
         return tx, y
 
-    def sample_points_baseline(self, n_batch, point_base, ws):
+    def sample_points_baseline(self, n_batch, point_base, ws, out=None):
         """Points at counters [point_base, point_base + n) sampled inside the per-point baseline
         launch (dpi_sample_points_baseline) into ws (uint8, >= workspace_bytes): tx (n, 1+nx), bitwise
-        sample_t_and_x's, and the baseline point_baseline would leave in ws."""
+        sample_t_and_x's, and the baseline point_baseline would leave in ws.  out: the (n, 1+nx) fp32
+        tensor to write tx into."""
         n, F = n_batch, 1 + self.equation.nx
         if ws.numel() < self.workspace_bytes(n, max(self.n_estimate_terminal, self.n_estimate_integral)):
             raise ValueError("workspace too small")
-        tx = torch.empty(n, F, dtype=torch.float32, device=self._device)
+        tx = torch.empty(n, F, dtype=torch.float32, device=self._device) if out is None else out
+        if tx.shape != (n, F) or tx.dtype != torch.float32 or not tx.is_contiguous() or tx.device != self._device:
+            raise ValueError("out must be a contiguous (n, 1+nx) fp32 tensor on the generator's device")
         self._configure_problem()
         _lib.check(self.lib.dpi_sample_points_baseline(self.problem, self.net.handle, n, self.seed, self.epoch,
                                                        point_base, self.eps, self.t_factors, _ptr(tx), _ptr(ws),

@@ -144,18 +144,28 @@ class ShardedLabeler:
         with torch.cuda.stream(self._side):
             if self._prep_free[k] is not None:  # the batch that last used this workspace is finalized
                 self._side.wait_event(self._prep_free[k])
+            m0, m1 = self.shard(M)
             if ahead is not None:
                 tx, pb, ev = ahead[3:]
                 self._side.wait_event(ev)
                 tx.record_stream(self._side)
-            elif hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
-                pb = gen._take_points(n)
-                tx = gen.sample_points_baseline(n, pb, ws)
+                gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
+            elif pis or not hasattr(gen, "sample_points_baseline"):  # the staged rollout reads the points
+                if hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
+                    pb = gen._take_points(n)
+                    tx = gen.sample_points_baseline(n, pb, ws)
+                else:
+                    tx, pb = gen.sample_t_and_x(n)
+                    gen.point_baseline(tx, ws=ws)
+                gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
             else:
-                tx, pb = gen.sample_t_and_x(n)
-                gen.point_baseline(tx, ws=ws)
-            m0, m1 = self.shard(M)
-            gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
+                # fused-kernel nets: the staged part (GBM: the noise sums, dpi_label_prepare) needs no
+                # points, so it is enqueued first and starts beside the previous batch's path launch;
+                # the sampling + baseline launch follows it on this stream
+                pb = gen._take_points(n)
+                tx = torch.empty(n, 1 + gen.equation.nx, dtype=torch.float32, device=gen.device)
+                gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
+                gen.sample_points_baseline(n, pb, ws, out=tx)
             ready = torch.cuda.Event()
             ready.record(self._side)
         tx.record_stream(cur)

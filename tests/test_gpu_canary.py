@@ -115,6 +115,9 @@ FIRST_ORDER = {
     "gbm_sdgd": ("gbm_sdgd", 3, 192, 0, 192, L.DPI_BOTH, True, False, 0.0),
     "gbm_sdgd_shard": ("gbm_sdgd", 3, 256, 64, 192, L.DPI_BOTH, False, False, 0.0),
     "gbm_td": ("gbm_sdgd", 2, 128, 0, 128, L.DPI_BOTH, True, False, 0.4),
+    # the noise sums staged by dpi_label_prepare (k_noise_shared) into the workspace, then read
+    "gbm_prepared": ("gbm_sdgd", 3, 192, 0, 192, L.DPI_BOTH, True, True, 0.0),
+    "gbm_prepared_shard": ("gbm_sdgd", 5, 256, 64, 192, L.DPI_BOTH, False, True, 0.0),
     "pis_partial_tile": ("pis", 3, 64, 0, 64, L.DPI_BOTH, True, False, 0.0),
     "pis_shard_m0": ("pis", 3, 256, 64, 192, L.DPI_BOTH, False, False, 0.0),
     "pis_prepared": ("pis", 5, 128, 0, 128, L.DPI_BOTH, True, True, 0.0),

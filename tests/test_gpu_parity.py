@@ -553,7 +553,7 @@ def test_label_call_captures_into_a_hip_graph(kind):
         assert torch.equal(y, eager)
 
 
-@pytest.mark.parametrize("kind", ["cha_mlp", "ou_pis"])
+@pytest.mark.parametrize("kind", ["cha_mlp", "ou_pis", "gbm_sdgd", "gbm_sdgd_tanh", "gbm_full_f32"])
 def test_side_stream_preparation_equals_labels(kind):
     """bench.py's pipeline: ShardedLabeler.prepare (sampling + per-point baseline on a side stream,
     three rotating workspaces) -> begin -> end, with one batch in flight, gives every batch's labels
@@ -563,15 +563,25 @@ def test_side_stream_preparation_equals_labels(kind):
 
     def make():
         torch.manual_seed(4)
+        hess = None
         if kind == "cha_mlp":
             eq = dpi.Cha(100, 1.0, 5.0, 1.0)
             net = _random_mlp(eq, [128] * 4, 4)
+        elif kind.startswith("gbm"):  # the noise sums staged by k_noise_shared (dpi_label_prepare)
+            eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+            torch.manual_seed(4)
+            net = dpi.construct_mlp(101, 1, [64] * 3, ["Tanh" if kind.endswith("tanh") else "ELU"] * 3, None)
+            hess = None if kind == "gbm_full_f32" else {"method": "SDGD", "kwargs": {"v": 100}}
         else:
             eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
                                        alpha_scale=4.0)
             net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
-        return dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True,
-                                       n_estimate_terminal=256, n_estimate_integral=256, n_euler_steps=6, seed=3)
+        gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True,
+                                      n_estimate_terminal=256, n_estimate_integral=256, n_euler_steps=6, seed=3,
+                                      hessian_approximation=hess)
+        if kind.endswith("f32"):
+            gen.net.set_precision(0)
+        return gen
 
     lab, ref = ShardedLabeler(make()), ShardedLabeler(make())
     got, pending = [], []

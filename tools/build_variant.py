@@ -22,7 +22,7 @@ for u in units:
     obj = out_dir / f"{Path(u).stem}_{name}.o"
     subprocess.run([B.HIPCC, *B.FLAGS, *defs, "-c", "-o", str(obj), str(B.CSRC / u)], check=True)
     objs.append(obj)
-objs += [B.OBJ / (Path(u).stem + ".o") for u in B.UNITS if u not in units]
+objs += [B.OBJ / (Path(u).stem + ".o") for u in B.UNITS if u not in units] + [B.OBJ / "dpi_build_id.o"]
 so = out_dir / f"libdpi_{name}.so"
 subprocess.run([B.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(so), *map(str, objs)], check=True)
 print(so)
