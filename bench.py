@@ -238,7 +238,10 @@ def main():
         args.workload = "burgers" if world == 1 else "burgers_cfg3"
     # PISGradNet (hjb): the next batch's rollout runs on the side stream beside this batch's k_pis_net,
     # one wave per SIMD (k_pis_rollout_shared) — the default for that workload
-    args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis"))) and not args.no_prepare
+    # GBM (configs[4], first-order labels): the next batch's noise sums (k_noise_shared, one wave per
+    # SIMD) beside this batch's network launch — 0.768 -> 0.735 ms/step (profiles/r05d_bench_gbm_*)
+    args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis") or args.workload == "gbm")) \
+        and not args.no_prepare
     if args.prepare and os.environ.get("DPI_BENCH_MAIN_PRIORITY", "high") == "high":
         lo, hi = torch.cuda.Stream.priority_range()
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=hi))

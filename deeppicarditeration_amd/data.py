@@ -422,8 +422,8 @@ class OnlineDataGenerator:
         if ws.numel() < self.workspace_bytes(n, max(self.n_estimate_terminal, self.n_estimate_integral)):
             raise ValueError("workspace too small")
         tx = torch.empty(n, F, dtype=torch.float32, device=self._device) if out is None else out
-        if tx.shape != (n, F) or tx.dtype != torch.float32 or not tx.is_contiguous() or tx.device != self._device:
-            raise ValueError("out must be a contiguous (n, 1+nx) fp32 tensor on the generator's device")
+        if tx.shape != (n, F) or tx.dtype != torch.float32 or not tx.is_contiguous() or tx.device.type != "cuda":
+            raise ValueError("out must be a contiguous (n, 1+nx) fp32 GPU tensor")
         self._configure_problem()
         _lib.check(self.lib.dpi_sample_points_baseline(self.problem, self.net.handle, n, self.seed, self.epoch,
                                                        point_base, self.eps, self.t_factors, _ptr(tx), _ptr(ws),
