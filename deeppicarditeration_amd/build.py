@@ -1,7 +1,7 @@
 """Build libdpi_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
 
-Ten translation units (the C-ABI / PIS / reduce TU, one k_paths family per equation, one
-TD-estimator k_paths family per equation and one Tanh-activation family per equation) compile in parallel to objects, then link into one
+Thirteen translation units (the C-ABI / PIS / reduce TU, and per equation the k_paths family, its
+TD-estimator family and the Tanh-activation twins of both) compile in parallel to objects, then link into one
 shared library together with a generated one-function unit, `dpi_build_id()`, that returns the
 SHA-256 of the sources and flags (`source_hash`).  The same hash goes into `libdpi_hip.so.buildid`
 beside the library: a build is current when that file matches the tree's hash (not by mtime), and
@@ -18,7 +18,7 @@ REPO = ROOT.parent
 CSRC = ROOT / "csrc"
 UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_gbm.hip", "dpi_paths_td_cha.hip",
          "dpi_paths_td_ou.hip", "dpi_paths_td_gbm.hip", "dpi_paths_cha_tanh.hip", "dpi_paths_ou_tanh.hip",
-         "dpi_paths_gbm_tanh.hip"]
+         "dpi_paths_gbm_tanh.hip", "dpi_paths_td_cha_tanh.hip", "dpi_paths_td_ou_tanh.hip", "dpi_paths_td_gbm_tanh.hip"]
 OBJ = ROOT / "build"
 OUT = ROOT / "libdpi_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

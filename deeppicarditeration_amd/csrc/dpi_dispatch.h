@@ -148,3 +148,6 @@ bool dispatch_td_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch&
 bool dispatch_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_td_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

@@ -91,15 +91,25 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
   }
 }
 
-// Hessian block sums [n][nbp][C] -> y[:, off:off+C] = clip(sum / M): one wave per (point, column),
-// the canonical tree over blocks.
-__global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int C, int nbp,
+// Offset of Hessian element (d1, d2) in one packed group sum of k_paths' Hessian labels
+// (hess_tree_store): upper-triangle 16 x 16 tiles of an NT x NT tiling in row order, tile element
+// (r, c) at (r & 3) 64 + (r >> 2) 16 + c; (d1, d2) and (d2, d1) read the same word (symmetric labels).
+__device__ __forceinline__ int hess_packed_off(int d1, int d2, int NT) {
+  const int a = min(d1, d2), b = max(d1, d2);
+  const int I = a >> 4, J = b >> 4, r = a & 15, c = b & 15;
+  const int q = I * NT - ((I * (I - 1)) >> 1) + (J - I);
+  return q * 256 + (r & 3) * 64 + (r >> 2) * 16 + c;
+}
+
+// Hessian group sums [n][ng][TC] (packed) -> hsum [n][nx*nx], y[:, off:off+C] = clip(sum / M): one
+// wave per (point, column), the canonical tree over the groups (whose sums are the tree's subtrees).
+__global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int nx, int NT, int ng,
                                                      float* __restrict__ hsum, float invM, float bound,
                                                      float* __restrict__ y, int ystride, int yoff, int* status) {
-  const int i = blockIdx.y;
+  const int i = blockIdx.y, C = nx * nx, TC = NT * (NT + 1) / 2 * 256;
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  const float s = tree_sum(hpart + (size_t)i * nbp * C + c, nbp, (size_t)C);
+  const float s = tree_sum(hpart + (size_t)i * ng * TC + hess_packed_off(c / nx, c % nx, NT), ng, (size_t)TC);
   if ((threadIdx.x & 63) == 0) {
     flag_nonfinite(status, s);
     if (hsum) hsum[(size_t)i * C + c] = s;
@@ -107,19 +117,19 @@ __global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ h
   }
 }
 
-// The same sums for nbp <= 64 with one THREAD per (point, column): consecutive threads read
-// consecutive columns (coalesced; the wave-per-column form above reads 16 floats 40 KB apart per
-// wave), and the 64-leaf tree runs in registers — for nbp <= 64, tree_sum is exactly the perfect
+// The same sums for ng <= 64 with one THREAD per (point, column): consecutive threads read
+// neighbouring words of a tile row (the wave-per-column form above reads 16 floats a group apart per
+// wave), and the 64-leaf tree runs in registers — for ng <= 64, tree_sum is exactly the perfect
 // binary tree over 64 zero-padded leaves, so the results are bitwise those of k_reduce_hess.
-__global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__ hpart, int n, int C, int nbp,
+__global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__ hpart, int n, int nx, int NT, int ng,
                                                        float* __restrict__ hsum, float invM, float bound,
                                                        float* __restrict__ y, int ystride, int yoff, int* status) {
-  const int i = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x, C = nx * nx, TC = NT * (NT + 1) / 2 * 256;
   if (c >= C) return;
-  const float* p = hpart + (size_t)i * nbp * C + c;
+  const float* p = hpart + (size_t)i * ng * TC + hess_packed_off(c / nx, c % nx, NT);
   float v[64];
 #pragma unroll
-  for (int b = 0; b < 64; ++b) v[b] = b < nbp ? p[(size_t)b * C] : 0.f;
+  for (int b = 0; b < 64; ++b) v[b] = b < ng ? p[(size_t)b * TC] : 0.f;
 #pragma unroll
   for (int w = 1; w < 64; w <<= 1)
 #pragma unroll
@@ -1250,11 +1260,11 @@ static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Lau
   if (net->d.kind == 1 && net->d.act == DPI_ACT_TANH && !q.baseline) {  // the Tanh k_paths units
     switch (p->e.kind) {
       case DPI_EQ_CHA:
-        return dispatch_cha_tanh(p, net, q);
+        return td ? dispatch_td_cha_tanh(p, net, q) : dispatch_cha_tanh(p, net, q);
       case DPI_EQ_OU:
-        return dispatch_ou_tanh(p, net, q);
+        return td ? dispatch_td_ou_tanh(p, net, q) : dispatch_ou_tanh(p, net, q);
       case DPI_EQ_GBM:
-        return dispatch_gbm_tanh(p, net, q);
+        return td ? dispatch_td_gbm_tanh(p, net, q) : dispatch_gbm_tanh(p, net, q);
       default:
         return false;
     }
@@ -1785,9 +1795,18 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
 }
 
 // ---- Malliavin Hessian labels (generate_with_gradients_and_hessians)
-static size_t hess_extra(int n, int M, int nx, size_t* moff) {
-  const size_t nbp = (size_t)(M + P - 1) / P;
-  *moff = al256((size_t)n * nbp * nx * nx * 4);  // Hessian block sums, then the moments
+// Hessian-label grouping: G consecutive 64-path blocks per workgroup (k_paths, hess_tree_store)
+static int hess_group(int nbp) { return nbp >= 4 ? 4 : nbp >= 2 ? 2 : 1; }
+static int hess_tiles(int nx) {
+  const int NT = (nx + 15) / 16;
+  return NT * (NT + 1) / 2;
+}
+// [packed group sums n x ng x TC | scratch: 2 slots x 9 x 256 float4 per workgroup | moments]
+static size_t hess_extra(int n, int M, int nx, size_t* moff, size_t* soff = nullptr) {
+  const int nbp = (M + P - 1) / P, ng = (nbp + hess_group(nbp) - 1) / hess_group(nbp);
+  const size_t sums = al256((size_t)n * ng * hess_tiles(nx) * 256 * 4);
+  if (soff) *soff = sums;
+  *moff = sums + al256((size_t)n * ng * 2 * 9216 * 4);
   return *moff + al256((size_t)n * 2 * (1 + nx) * 4);
 }
 
@@ -1812,8 +1831,8 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "Hessian labels: at most DPI_PATHS_PER_CALL_MAX paths per call");
   const WsLayout w = ws_layout(net, n, M, F);
-  size_t moff;
-  const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);
+  size_t moff, soff;
+  const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff, &soff);
   if (ws_bytes < need) return fail(DPI_ERR_WORKSPACE, "workspace too small (dpi_workspace_bytes_hessians)");
   char* b = (char*)ws;
   PathArgs a;
@@ -1840,20 +1859,26 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.split = mlp_split(net) ? 1 : 0;  // fp16-split tangent sweeps (mlp_hdiag_split) unless DPI_GEMM_F32
   a.point_base = point_base;
   a.hpart = (float*)(b + base);
+  a.hscr = (float*)(b + base + soff);
+  a.hgroup = hess_group(nbp);
+  a.hgroups = (nbp + a.hgroup - 1) / a.hgroup;
+  const int NT = (nx + 15) / 16, ng = a.hgroups;
   hipStream_t st = (hipStream_t)stream;
-  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
+  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * ng, st};
   q.hess = true;
-  if (!dispatch_any(p, net, q))
-    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
-  HIPCHK(hipGetLastError());
+  for (a.hsb = 0; a.hsb < a.hgroup; ++a.hsb) {  // sub-block hsb of every group; the trees combine in order
+    if (!dispatch_any(p, net, q))
+      return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
+    HIPCHK(hipGetLastError());
+  }
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
                      1.0f / (float)M, 1, bound, y, F + C, net_status(net));
-  if (nbp <= 64)
-    hipLaunchKernelGGL(k_reduce_hess64, dim3((C + 255) / 256, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
-                     1.0f / (float)M, bound, y, F + C, F, net_status(net));
+  if (ng <= 64)
+    hipLaunchKernelGGL(k_reduce_hess64, dim3((C + 255) / 256, n), dim3(256), 0, st, a.hpart, n, nx, NT, ng, hsum,
+                       1.0f / (float)M, bound, y, F + C, F, net_status(net));
   else
-    hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, C, nbp, hsum,
-                     1.0f / (float)M, bound, y, F + C, F, net_status(net));
+    hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, nx, NT, ng, hsum,
+                       1.0f / (float)M, bound, y, F + C, F, net_status(net));
   HIPCHK(hipGetLastError());
   return 0;
 }

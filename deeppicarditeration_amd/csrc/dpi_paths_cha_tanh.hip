@@ -1,8 +1,8 @@
-// k_paths instantiations for DPI_EQ_CHA networks with Tanh hidden activations (plain and TD
-// estimators; torch.nn.Tanh, the reference's default NETWORK.ACTIVATIONS, picard/config.py:61).
+// k_paths instantiations for DPI_EQ_CHA networks with Tanh hidden activations (torch.nn.Tanh, the
+// reference's default NETWORK.ACTIVATIONS, picard/config.py:61); the TD estimators in
+// dpi_paths_td_cha_tanh.hip.
 #include "dpi_dispatch.h"
 
 bool dispatch_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
-  return q.td ? dpi_dispatch<DPI_EQ_CHA, true, DPI_ACT_TANH>(p, net, q)
-              : dpi_dispatch<DPI_EQ_CHA, false, DPI_ACT_TANH>(p, net, q);
+  return dpi_dispatch<DPI_EQ_CHA, false, DPI_ACT_TANH>(p, net, q);
 }
