@@ -138,6 +138,18 @@ class RangeGroup:
             self.calls = []
             self.gen._release_slot(self.slot)
 
+    def __del__(self):
+        # a group dropped unverified gives its slot back; should one of its kernels still flag into
+        # the slot after a later group has taken it, that group merely recomputes in fp32
+        try:
+            if not self.done:
+                self.done = True
+                if self.gen._scope is self:
+                    self.gen._scope = None
+                self.gen._release_slot(self.slot)
+        except Exception:
+            pass
+
     def __enter__(self):
         return self
 

@@ -58,9 +58,12 @@ class LabelBuffer:
                 txs.append(tx)
                 ys.append(y)
                 done += n
-        finally:
+        except BaseException:
             if grp is not None:
-                grp.close()
+                grp.discard()
+            raise
+        if grp is not None:
+            grp.close()
         if grp is not None:
             grp.verify()  # before the concatenation: a repair rewrites the calls' own outputs
         return torch.cat(txs), torch.cat(ys)
