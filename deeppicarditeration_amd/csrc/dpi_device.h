@@ -1541,13 +1541,9 @@ struct PathArgs {
   uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
   int order;  // phase order policy (k_paths)
   int split;  // fused MLP on the fp16-split MFMA
-  // Hessian labels: the hgroup (1, 2 or 4) consecutive 64-path blocks of a group run in hgroup
-  // launches (sub-block hsb) whose Hessian sums combine in the canonical tree ((b0 + b1) + (b2 + b3))
-  // through the group's two scratch slots (hscr); the group sum goes out once, as packed
-  // upper-triangle 16 x 16 tiles: hpart [n][hgroups][NT (NT + 1) / 2][256]
+  // Hessian labels: every block's sums as packed upper-triangle 16 x 16 tiles,
+  // hpart [n][nbp][NT (NT + 1) / 2][256] (hess_store)
   float* hpart;
-  float* hscr;
-  int hgroup, hgroups, hsb;
   uint32_t c3h1, c3h2;     // Hessian labels: Malliavin normal streams (tags HTERM, HINT)
   // DATA.ESTIMATE_DELTA_T (data.py:1209-1213): > 0 selects the TD estimators (k_paths<.., TD>),
   // horizon t_next = min(t + td_dt, T), terminal value u(t_next, X) where t_next < T
@@ -1636,41 +1632,19 @@ __global__ __launch_bounds__(64, 8) __attribute__((amdgpu_num_vgpr(24))) void k_
 // N1, N2: fresh normals (tags HTERM / HINT, k = 0), written into the noise tile in turn; the
 // outer-product sums are (nx x 64) (64 x nx) products on v_mfma_f32_16x16x4_f32 over the upper
 // triangle of 16 x 16 tiles (wave w owns tiles w, w+4, ...), mirrored on store.
-// Block sums of a Hessian-label workgroup's G sub-blocks in the canonical tree ((b0 + b1) + (b2 +
-// b3)) — the order k_reduce_hess's perfect tree gives the same blocks, so the labels and every
-// power-of-two MC sharding stay bitwise what one block per workgroup gave — through the
-// workgroup's two scratch slots (each lane stores and reloads only its own 16-B words: program
-// order, no barrier); then the group sum goes out once as packed upper-triangle tiles, tile q's
-// element (r, c) at q 256 + (r & 3) 64 + (r >> 2) 16 + c, one 256-B run per store instruction.
-// A sub-block past the call's blocks (a partial last group) enters as zeros, as the tree's padding.
-__device__ __forceinline__ void hess_tree_store(const PathArgs& a, floatx4 (&acc)[9], int NT, int sb, int G) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+// A block's Hessian sums out as packed upper-triangle tiles (the lower triangle is the mirror):
+// tile q's element (r, c) at q 256 + (r & 3) 64 + (r >> 2) 16 + c, one 256-B run per store
+// instruction — 28 tiles, 28 KB per block at nx = 100 against 40 KB for the full square.
+__device__ __forceinline__ void hess_store(const PathArgs& a, const floatx4 (&acc)[9], int NT) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ntiles = NT * (NT + 1) / 2;
-  float4* s0 = reinterpret_cast<float4*>(a.hscr + (size_t)blockIdx.x * 2 * 9216) + tid;
-  float4* s1 = s0 + 9 * 256;
-  auto ld = [](const float4* p) { return floatx4{p->x, p->y, p->z, p->w}; };
-  auto st = [](float4* p, const floatx4& v) { *p = make_float4(v[0], v[1], v[2], v[3]); };
   float* out = a.hpart + (size_t)blockIdx.x * ntiles * 256;
 #pragma unroll
   for (int sl = 0; sl < 9; ++sl) {
     const int q = wv + 4 * sl;
-    if (q >= ntiles) continue;
-    floatx4 v = acc[sl];
-    bool fin = false;
-    if (G == 1) {
-      fin = true;
-    } else if (G == 2) {
-      if (sb == 0) st(s0 + 256 * sl, v);
-      else v = ld(s0 + 256 * sl) + v, fin = true;
-    } else {
-      if (sb == 0) st(s0 + 256 * sl, v);
-      else if (sb == 1) st(s0 + 256 * sl, ld(s0 + 256 * sl) + v);
-      else if (sb == 2) st(s1 + 256 * sl, v);
-      else v = ld(s0 + 256 * sl) + (ld(s1 + 256 * sl) + v), fin = true;
-    }
-    if (fin)
+    if (q < ntiles)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) out[q * 256 + rr * 64 + lane] = v[rr];
+      for (int rr = 0; rr < 4; ++rr) out[q * 256 + rr * 64 + lane] = acc[sl][rr];
   }
 }
 
@@ -1699,7 +1673,7 @@ __device__ __forceinline__ void hess_accum(LdsGbm<H>& sh, const float* wgt, int 
 template <int KIND, int H, int L, bool ZERO, bool SPLIT, int ACT>
 __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, const PathArgs& a, LdsGbm<H>& sh,
                                            int i, int blk, uint32_t ig, uint32_t m, float s, float smt, float tmt,
-                                           float g_x, int nxp, int sb, int G) {
+                                           float g_x, int nxp) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, jj = lane & 15, qq = lane >> 4, pp = 16 * wv + jj;
   const int nx = e.nx, F = 1 + nx, nb = (nx + 3) >> 2, NT = nxp / 16;
   // f at (s, x + cmul S) with the full Hessian diagonal (get_f without SDGD, data.py:1262-1272);
@@ -1819,7 +1793,7 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
   __syncthreads();
   hess_accum<H, L>(sh, wgt, NT, acc);
 
-  // ---- identity part, then this sub-block's place in the group's tree
+  // ---- identity part
   const float dsum = wave_sum(aI + aT);
   const int ntiles = NT * (NT + 1) / 2;
 #pragma unroll
@@ -1839,7 +1813,7 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
       }
     }
   }
-  hess_tree_store(a, acc, NT, sb, G);
+  hess_store(a, acc, NT);
 }
 
 
@@ -1903,27 +1877,15 @@ __device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, co
   if (threadIdx.x == 0) a.tickets[i] = 0;
 }
 
-// The path launch: one workgroup per (point, 64-path block).  For the Hessian labels the call runs
-// it hgroup times (sub-block index a.hsb): workgroup (i, g) of launch sb takes block g hgroup + sb
-// of point i and enters its Hessian sums into the (i, g) group's tree (hess_tree_store), so the
-// block-sum slab holds hgroups rows per point instead of nbp.
+// The path launch: one workgroup per (point, 64-path block).
 template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
 __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
-  const int i = HESS ? blockIdx.x / a.hgroups : blockIdx.x / a.nbp;
-  const int blk = HESS ? (blockIdx.x - i * a.hgroups) * a.hgroup + a.hsb : blockIdx.x - i * a.nbp;
-  if constexpr (HESS) {
-    if (blk >= a.nbp) {  // past the call's blocks (a partial last group): zeros in the group's tree
-      floatx4 z[9];
-#pragma unroll
-      for (int sl = 0; sl < 9; ++sl) z[sl] = floatx4{0.f, 0.f, 0.f, 0.f};
-      hess_tree_store(a, z, (ZERO ? ((e.nx + 15) & ~15) : net.nxp) / 16, a.hsb, a.hgroup);
-      return;
-    }
-  }
+  const int i = blockIdx.x / a.nbp;
+  const int blk = blockIdx.x - i * a.nbp;
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
   // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM; round 4: GBM 8, Hessian labels 4)
@@ -2329,7 +2291,7 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
     }
   }
   if constexpr (HESS) {
-    hess_block<KIND, H, L, ZERO, SPLIT, ACT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp, a.hsb, a.hgroup);
+    hess_block<KIND, H, L, ZERO, SPLIT, ACT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
   } else {
     if (a.tickets) fused_reduce(a, i, F, out);
   }

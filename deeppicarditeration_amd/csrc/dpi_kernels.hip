@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void k_reduce(const float* __restrict__ partia
 }
 
 // Offset of Hessian element (d1, d2) in one packed group sum of k_paths' Hessian labels
-// (hess_tree_store): upper-triangle 16 x 16 tiles of an NT x NT tiling in row order, tile element
+// (hess_store): upper-triangle 16 x 16 tiles of an NT x NT tiling in row order, tile element
 // (r, c) at (r & 3) 64 + (r >> 2) 16 + c; (d1, d2) and (d2, d1) read the same word (symmetric labels).
 __device__ __forceinline__ int hess_packed_off(int d1, int d2, int NT) {
   const int a = min(d1, d2), b = max(d1, d2);
@@ -101,42 +101,80 @@ __device__ __forceinline__ int hess_packed_off(int d1, int d2, int NT) {
   return q * 256 + (r & 3) * 64 + (r >> 2) * 16 + c;
 }
 
-// Hessian group sums [n][ng][TC] (packed) -> hsum [n][nx*nx], y[:, off:off+C] = clip(sum / M): one
-// wave per (point, column), the canonical tree over the groups (whose sums are the tree's subtrees).
-__global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int nx, int NT, int ng,
-                                                     float* __restrict__ hsum, float invM, float bound,
-                                                     float* __restrict__ y, int ystride, int yoff, int* status) {
-  const int i = blockIdx.y, C = nx * nx, TC = NT * (NT + 1) / 2 * 256;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;
-  const float s = tree_sum(hpart + (size_t)i * ng * TC + hess_packed_off(c / nx, c % nx, NT), ng, (size_t)TC);
-  if ((threadIdx.x & 63) == 0) {
-    flag_nonfinite(status, s);
-    if (hsum) hsum[(size_t)i * C + c] = s;
-    if (y) y[(size_t)i * ystride + yoff + c] = clip_label(s * invM, bound);
+// tree_sum's canonical order in ONE thread: the perfect binary tree, left + right at every level,
+// over cnt values zero-padded to P2 = max(64, 2^ceil(log2 cnt)) leaves — bitwise tree_sum's result
+// (and every power-of-two sharding of the leaves still reproduces it).  Up to 64 leaves the tree
+// runs unrolled in registers; beyond, as a binary counter over the leaves (level l holds the left
+// subtree of 2^l leaves until its right sibling completes).
+__device__ __forceinline__ float thread_tree(const float* __restrict__ p, int cnt, size_t stride) {
+  if (cnt <= 64) {
+    float v[64];
+#pragma unroll
+    for (int b = 0; b < 64; ++b) v[b] = b < cnt ? p[(size_t)b * stride] : 0.f;
+#pragma unroll
+    for (int w = 1; w < 64; w <<= 1)
+#pragma unroll
+      for (int b = 0; b < 64; b += 2 * w) v[b] = v[b] + v[b + w];
+    return v[0];
   }
+  int p2 = 64;
+  while (p2 < cnt) p2 <<= 1;
+  float st[16], x = 0.f;
+#pragma unroll
+  for (int l = 0; l < 16; ++l) st[l] = 0.f;
+#pragma unroll 4
+  for (int b = 0; b < p2; ++b) {
+    x = b < cnt ? p[(size_t)b * stride] : 0.f;
+    bool carry = true;
+#pragma unroll
+    for (int l = 0; l < 16; ++l)
+      if (carry) {
+        if ((b >> l) & 1) {
+          x = st[l] + x;
+        } else {
+          st[l] = x;
+          carry = false;
+        }
+      }
+  }
+  return x;  // the last leaf's carry reached the root
 }
 
-// The same sums for ng <= 64 with one THREAD per (point, column): consecutive threads read
-// neighbouring words of a tile row (the wave-per-column form above reads 16 floats a group apart per
-// wave), and the 64-leaf tree runs in registers — for ng <= 64, tree_sum is exactly the perfect
-// binary tree over 64 zero-padded leaves, so the results are bitwise those of k_reduce_hess.
-__global__ __launch_bounds__(256) void k_reduce_hess64(const float* __restrict__ hpart, int n, int nx, int NT, int ng,
-                                                       float* __restrict__ hsum, float invM, float bound,
-                                                       float* __restrict__ y, int ystride, int yoff, int* status) {
-  const int i = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x, C = nx * nx, TC = NT * (NT + 1) / 2 * 256;
-  if (c >= C) return;
-  const float* p = hpart + (size_t)i * ng * TC + hess_packed_off(c / nx, c % nx, NT);
-  float v[64];
-#pragma unroll
-  for (int b = 0; b < 64; ++b) v[b] = b < ng ? p[(size_t)b * TC] : 0.f;
-#pragma unroll
-  for (int w = 1; w < 64; w <<= 1)
-#pragma unroll
-    for (int b = 0; b < 64; b += 2 * w) v[b] = v[b] + v[b + w];
-  flag_nonfinite(status, v[0]);
-  if (hsum) hsum[(size_t)i * C + c] = v[0];
-  if (y) y[(size_t)i * ystride + yoff + c] = clip_label(v[0] * invM, bound);
+// Hessian block sums [n][nbp][TC] (packed upper-triangle tiles, hess_packed_off) -> hsum [n][nx*nx]
+// and y[:, off:off+C] = clip(sum / M).  One thread per packed word: consecutive threads read
+// consecutive words of every block (each word read once), sum them in the canonical tree over the
+// blocks (thread_tree = tree_sum's order), and store the result at (d1, d2) and (d2, d1) (the
+// diagonal tiles' lower halves are skipped: (d1, d2) and (d2, d1) take the upper element, as
+// hess_packed_off maps them).  Workgroups are mapped XCD-major: workgroup b runs on XCD b % 8, and an
+// XCD's workgroups take whole points (bpp workgroups each), so a point's transposed stores merge
+// in one L2 instead of leaving eight XCDs as partial lines.
+__global__ __launch_bounds__(256) void k_reduce_hess(const float* __restrict__ hpart, int n, int nx, int NT, int nbp,
+                                                     int bpp, float* __restrict__ hsum, float invM, float bound,
+                                                     float* __restrict__ y, int ystride, int yoff, int* status) {
+  const int TC = NT * (NT + 1) / 2 * 256, C = nx * nx;
+  const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+  const int i = (k / bpp) * 8 + xcd, w = (k % bpp) * 256 + threadIdx.x;
+  if (i >= n || w >= TC) return;
+  const int q = w >> 8, e = w & 255, r = ((e >> 4) & 3) * 4 + (e >> 6), c = e & 15;
+  int I = 0, rq = q;
+  while (rq >= NT - I) {
+    rq -= NT - I;
+    ++I;
+  }
+  const int J = I + rq, d1 = 16 * I + r, d2 = 16 * J + c;
+  if (d1 >= nx || d2 >= nx || (I == J && r > c)) return;
+  const float s = thread_tree(hpart + (size_t)i * nbp * TC + w, nbp, (size_t)TC);
+  flag_nonfinite(status, s);
+  const float v = clip_label(s * invM, bound);
+  const size_t o1 = (size_t)d1 * nx + d2, o2 = (size_t)d2 * nx + d1;
+  if (hsum) {
+    hsum[(size_t)i * C + o1] = s;
+    hsum[(size_t)i * C + o2] = s;
+  }
+  if (y) {
+    y[(size_t)i * ystride + yoff + o1] = v;
+    y[(size_t)i * ystride + yoff + o2] = v;
+  }
 }
 
 // Hessian sums (n, C) -> y[:, off:off+C] = clip(sum / M)
@@ -1795,18 +1833,14 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
 }
 
 // ---- Malliavin Hessian labels (generate_with_gradients_and_hessians)
-// Hessian-label grouping: G consecutive 64-path blocks per workgroup (k_paths, hess_tree_store)
-static int hess_group(int nbp) { return nbp >= 4 ? 4 : nbp >= 2 ? 2 : 1; }
 static int hess_tiles(int nx) {
   const int NT = (nx + 15) / 16;
   return NT * (NT + 1) / 2;
 }
-// [packed group sums n x ng x TC | scratch: 2 slots x 9 x 256 float4 per workgroup | moments]
-static size_t hess_extra(int n, int M, int nx, size_t* moff, size_t* soff = nullptr) {
-  const int nbp = (M + P - 1) / P, ng = (nbp + hess_group(nbp) - 1) / hess_group(nbp);
-  const size_t sums = al256((size_t)n * ng * hess_tiles(nx) * 256 * 4);
-  if (soff) *soff = sums;
-  *moff = sums + al256((size_t)n * ng * 2 * 9216 * 4);
+// [packed block sums n x nbp x TC | moments]
+static size_t hess_extra(int n, int M, int nx, size_t* moff) {
+  const int nbp = (M + P - 1) / P;
+  *moff = al256((size_t)n * nbp * hess_tiles(nx) * 256 * 4);
   return *moff + al256((size_t)n * 2 * (1 + nx) * 4);
 }
 
@@ -1831,8 +1865,8 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "Hessian labels: at most DPI_PATHS_PER_CALL_MAX paths per call");
   const WsLayout w = ws_layout(net, n, M, F);
-  size_t moff, soff;
-  const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff, &soff);
+  size_t moff;
+  const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);
   if (ws_bytes < need) return fail(DPI_ERR_WORKSPACE, "workspace too small (dpi_workspace_bytes_hessians)");
   char* b = (char*)ws;
   PathArgs a;
@@ -1859,26 +1893,18 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.split = mlp_split(net) ? 1 : 0;  // fp16-split tangent sweeps (mlp_hdiag_split) unless DPI_GEMM_F32
   a.point_base = point_base;
   a.hpart = (float*)(b + base);
-  a.hscr = (float*)(b + base + soff);
-  a.hgroup = hess_group(nbp);
-  a.hgroups = (nbp + a.hgroup - 1) / a.hgroup;
-  const int NT = (nx + 15) / 16, ng = a.hgroups;
+  const int NT = (nx + 15) / 16;
   hipStream_t st = (hipStream_t)stream;
-  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * ng, st};
+  Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
   q.hess = true;
-  for (a.hsb = 0; a.hsb < a.hgroup; ++a.hsb) {  // sub-block hsb of every group; the trees combine in order
-    if (!dispatch_any(p, net, q))
-      return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
-    HIPCHK(hipGetLastError());
-  }
+  if (!dispatch_any(p, net, q))
+    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
+  HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
                      1.0f / (float)M, 1, bound, y, F + C, net_status(net));
-  if (ng <= 64)
-    hipLaunchKernelGGL(k_reduce_hess64, dim3((C + 255) / 256, n), dim3(256), 0, st, a.hpart, n, nx, NT, ng, hsum,
-                       1.0f / (float)M, bound, y, F + C, F, net_status(net));
-  else
-    hipLaunchKernelGGL(k_reduce_hess, dim3((C + 3) / 4, n), dim3(256), 0, st, a.hpart, n, nx, NT, ng, hsum,
-                       1.0f / (float)M, bound, y, F + C, F, net_status(net));
+  const int bpp = hess_tiles(nx);  // 256 packed words per workgroup: one 16 x 16 tile
+  hipLaunchKernelGGL(k_reduce_hess, dim3((unsigned)((n + 7) / 8) * 8 * bpp), dim3(256), 0, st, a.hpart, n, nx, NT, nbp,
+                     bpp, hsum, 1.0f / (float)M, bound, y, F + C, F, net_status(net));
   HIPCHK(hipGetLastError());
   return 0;
 }
