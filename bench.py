@@ -504,9 +504,17 @@ def main():
             busy_note = f", scaled by this rank's share of the paths ({M_PER_GPU}/{M})"
         if vf.exists() and not wl.get("pis"):
             kern = json.loads(vf.read_text())["kernels"]
-            # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD>: the network launch, not the u = 0 twin
-            net_k = [v for k, v in kern.items() if k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
-            busy = max(net_k, key=lambda v: v["dispatches"])["valu_busy_cycles_per_simd"] * scale
+            # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD, ACT>: the network launch, not the u = 0 twin
+            net_k = [v for k, v in kern.items()
+                     if "k_paths<" in k and k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
+            top = max(net_k, key=lambda v: v["dispatches"])
+            busy = top["valu_busy_cycles_per_simd"] * scale
+            # the GBM prepare schedule: the next batch's noise sums (k_noise_shared, prepare stream) issue
+            # on the same SIMDs during the network launch — their VALU issue per call counts too
+            noise_k = [v for k, v in kern.items() if "k_noise_shared<" in k]
+            if noise_k:
+                busy += sum(v["valu_busy_cycles_per_simd"] * v["dispatches"] for v in noise_k) / top["dispatches"] * scale
+                busy_note += ", plus the prepare stream's k_noise_shared issue per call (it runs inside the launch)"
             valu = {"achieved": busy * N_SIMD / (k_ms * 1e-3) / 1e12, "peak": N_SIMD * PEAK_CLOCK_GHZ * 1e9 / 1e12,
                     "unit": "T VALU-busy SIMD-cycles/s", "valu_busy_cycles_per_simd": busy,
                     "busy_source": f"profile_derived: {vf.relative_to(ROOT)} (SQ_ACTIVE_INST_VALU x 4 / "

@@ -41,7 +41,7 @@ for wl, anchor in ANCHOR.items():
             agg[r["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(r["Counter_Value"]))
         pmc[c] = {k: {"dispatches": len(v), "total_kb": sum(v)} for k, v in agg.items()}
         (dst / f"{tag}_pmc_{wl}_{c}.json").write_text(json.dumps(
-            {"command": f"rocprofv3 --pmc {c} --kernel-include-regex 'k_paths|k_pis|k_gemm|k_reduce' -- python "
+            {"command": f"rocprofv3 --pmc {c} --kernel-include-regex 'k_paths|k_pis|k_gemm|k_reduce|k_noise' -- python "
                         f"bench.py --workload {wl} --steps 10 --warmup 2 --no-cpu-baseline", "kernels": pmc[c]},
             indent=1))
     if len(pmc) < 2:
@@ -79,7 +79,7 @@ for wl in ("burgers", "burgers_cfg3", "gbm", "gbm_hess"):
     for (name, _), c in per.items():
         kinds[name].append(c)
     out = {"command": f"rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES "
-                      f"SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex k_paths -- python bench.py --workload {wl} "
+                      f"SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex 'k_paths|k_noise' -- python bench.py --workload {wl} "
                       "--steps 10 --warmup 2 --no-cpu-baseline",
            "units": "per launch; valu_busy_cycles_per_simd = SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs; kernel_cycles = "
                     "GRBM_GUI_ACTIVE / 8 XCDs; valu_busy = their ratio (the rocprofv3 VALUBusy expression)",
