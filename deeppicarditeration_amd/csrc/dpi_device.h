@@ -1276,6 +1276,20 @@ __device__ __forceinline__ float block_sum_b(float v, float* red) {
   return a;
 }
 
+// Phase stamps of k_baseline (measurement variant only, tools/base_stamps.py): thread 0 of each of
+// the first 512 blocks writes s_memtime at fixed points (after the barrier that closes a phase).
+#ifdef DPI_BASE_STAMPS
+__device__ unsigned long long dpi_bstamps[512 * 16];
+#define DPI_BSTAMP(ev)                                                                              \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 512) dpi_bstamps[blockIdx.x * 16 + (ev)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define DPI_BSTAMP(ev) \
+  do {                 \
+  } while (0)
+#endif
+
 // Baseline per point (one workgroup per point): g(x), the state-dependent part of
 // f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
 // f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
@@ -1295,6 +1309,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   __shared__ float ts;
   const int i = blockIdx.x, tid = threadIdx.x;
   const int nx = e.nx, F = 1 + nx;
+  DPI_BSTAMP(0);
   if (tickets && tid == 0) tickets[i] = 0;
   if (smp.tx) {
     const uint32_t ig = smp.point_base + (uint32_t)i;
@@ -1323,6 +1338,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
   }
   __syncthreads();
+  DPI_BSTAMP(1);
   const float t = ts;
   // g(x): per-thread dims, then per-statistic block sums in fixed order (one barrier pair)
   {
@@ -1347,6 +1363,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       gx[i] = Eq<KIND>::gfin(e, st);
     }
   }
+  DPI_BSTAMP(2);
   float Cb = 0.f;
   if constexpr (KIND == DPI_EQ_GBM) {
     // exact-solution part of ffi at (t, x) (equations.py:457-466); the NSG dot products w_c . x
@@ -1377,6 +1394,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     }
     const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
     Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
+    DPI_BSTAMP(3);
     if (ZERO) {
       for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
       if (tid == 0) fb[i] = Cb;
@@ -1426,12 +1444,13 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     if (tid < H) act[l][tid] = act_f(net.act, acc + net.b[l][tid]);
     __syncthreads();
   }
+  DPI_BSTAMP(4);
   if constexpr (KIND == DPI_EQ_GBM) {
     // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
     // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
     __shared__ float lamb[4][HMAX];
     __shared__ float cb[HMAX];
-    __shared__ float ztb[2][64][NXP_MAX];
+    __shared__ __attribute__((aligned(16))) float ztb[2][64][NXP_MAX];
     if (tid < H) lamb[L - 1][tid] = net.wout[tid];
     __syncthreads();
     // adjoints: lam_l = W_{l+1}^T (elu'(a_{l+1}) * lam_{l+1}), a k-sliced mat-vec over the block with
@@ -1443,19 +1462,38 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       if (tid < H) lamb[l][tid] = acc;
       __syncthreads();
     }
-    // Tangent sweep as an LDS mat-mat per layer: thread (d = tid % 128, hg = tid / 128) owns the
-    // rows h = hg + 8 j of the tangent Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k]) Z_{l-1}[k][d];
-    // k runs outermost in steps of 4, so one Z read serves all 8 rows and each row's 4 scaled
-    // weights come in one broadcast ds_read_b128 (every output is the same k-ascending fma chain).
+    DPI_BSTAMP(5);
+    // Tangent sweep as an LDS mat-mat per layer, Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k])
+    // Z_{l-1}[k][d]: thread t < 512 owns rows h = hg + 16 j (j < H / 16 <= 4) and columns
+    // d = 4 dg .. 4 dg + 3 (hg = t / 32, dg = t % 32), 16 accumulators.  k runs outermost in steps
+    // of 4: per step one float4 of Z per k and one broadcast float4 of scaled weights per row, a
+    // third of the LDS return bytes of the column-per-thread form, which was bound by them (2.4 MB
+    // per layer; 22 K cycles of the launch's 87 K, tools/base_stamps.py r05j).  Every output is the
+    // same k-ascending fma chain as before; only the row grouping of the u_dd partials changed.
     __shared__ __attribute__((aligned(16))) float wsc[64 * 64];
-    __shared__ float udp[8][NXP_MAX];
-    const int d = tid % NXP_MAX, hg = tid / NXP_MAX;  // NTHB = 8 x NXP_MAX
-    float ud = 0.f;
-    for (int h = hg; h < H; h += 8) {
-      const float z = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
-      ztb[0][h][d] = z;
-      ud = fmaf(lamb[0][h] * act_d2(net.act, act[0][h]), z * z, ud);
+    __shared__ float udp[16][NXP_MAX];
+    const bool sw = tid < 512;
+    const int dg = tid & 31, hg = (tid >> 5) & 15, RJ = (H + 15) >> 4;
+    float ud[4] = {0.f, 0.f, 0.f, 0.f};
+    if (sw) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = hg + 16 * j;
+        if (j < RJ && h < H) {
+          float z[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int d = 4 * dg + q;
+            z[q] = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
+          }
+          *reinterpret_cast<float4*>(&ztb[0][h][4 * dg]) = make_float4(z[0], z[1], z[2], z[3]);
+          const float c = lamb[0][h] * act_d2(net.act, act[0][h]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[q] * z[q], ud[q]);
+        }
+      }
     }
+    DPI_BSTAMP(6);
     int cz = 0;
     const int H4 = H & ~3;
     for (int l = 1; l < L; ++l) {
@@ -1464,46 +1502,70 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
         wsc[h * 64 + k] = net.W[l][q] * act_d(net.act, act[l - 1][k]);
       }
       __syncthreads();  // wsc and Z_{l-1} complete
-      float z[8];
+      if (sw) {
+        float z[4][4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) z[j] = 0.f;
-      for (int k = 0; k < H4; k += 4) {
-        const float z0 = ztb[cz][k][d], z1 = ztb[cz][k + 1][d], z2 = ztb[cz][k + 2][d], z3 = ztb[cz][k + 3][d];
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (hg + 8 * j < H) {
-            const float4 w = *reinterpret_cast<const float4*>(&wsc[(hg + 8 * j) * 64 + k]);
-            z[j] = fmaf(w.w, z3, fmaf(w.z, z2, fmaf(w.y, z1, fmaf(w.x, z0, z[j]))));
+          for (int q = 0; q < 4; ++q) z[j][q] = 0.f;
+#ifndef DPI_BASE_SWEEP_UNROLL
+#define DPI_BASE_SWEEP_UNROLL 1
+#endif
+        constexpr int SWU = DPI_BASE_SWEEP_UNROLL;  // measurement knob: k-steps unrolled
+#pragma unroll SWU
+        for (int k = 0; k < H4; k += 4) {
+          const float4 z0 = *reinterpret_cast<const float4*>(&ztb[cz][k][4 * dg]);
+          const float4 z1 = *reinterpret_cast<const float4*>(&ztb[cz][k + 1][4 * dg]);
+          const float4 z2 = *reinterpret_cast<const float4*>(&ztb[cz][k + 2][4 * dg]);
+          const float4 z3 = *reinterpret_cast<const float4*>(&ztb[cz][k + 3][4 * dg]);
+          const float a0[4] = {z0.x, z0.y, z0.z, z0.w}, a1[4] = {z1.x, z1.y, z1.z, z1.w};
+          const float a2[4] = {z2.x, z2.y, z2.z, z2.w}, a3[4] = {z3.x, z3.y, z3.z, z3.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < RJ && hg + 16 * j < H) {
+              const float4 w = *reinterpret_cast<const float4*>(&wsc[(hg + 16 * j) * 64 + k]);
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                z[j][q] = fmaf(w.w, a3[q], fmaf(w.z, a2[q], fmaf(w.y, a1[q], fmaf(w.x, a0[q], z[j][q]))));
+            }
+        }
+        for (int k = H4; k < H; ++k) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j < RJ && hg + 16 * j < H)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) z[j][q] = fmaf(wsc[(hg + 16 * j) * 64 + k], ztb[cz][k][4 * dg + q], z[j][q]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int h = hg + 16 * j;
+          if (j < RJ && h < H) {
+            *reinterpret_cast<float4*>(&ztb[cz ^ 1][h][4 * dg]) = make_float4(z[j][0], z[j][1], z[j][2], z[j][3]);
+            const float c = lamb[l][h] * act_d2(net.act, act[l][h]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[j][q] * z[j][q], ud[q]);
           }
-      }
-      for (int k = H4; k < H; ++k) {
-        const float zk = ztb[cz][k][d];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (hg + 8 * j < H) z[j] = fmaf(wsc[(hg + 8 * j) * 64 + k], zk, z[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int h = hg + 8 * j;
-        if (h < H) {
-          ztb[cz ^ 1][h][d] = z[j];
-          ud = fmaf(lamb[l][h] * act_d2(net.act, act[l][h]), z[j] * z[j], ud);
         }
       }
       cz ^= 1;
       __syncthreads();  // before wsc is overwritten
+      DPI_BSTAMP(6 + l);
     }
-    udp[hg][d] = ud;
+    if (sw)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) udp[hg][4 * dg + q] = ud[q];
     __syncthreads();
     if (tid < NXP_MAX) {
       float a = 0.f;
-      for (int g = 0; g < 8; ++g) a += udp[g][tid];
+      for (int g = 0; g < 16; ++g) a += udp[g][tid];
       hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
     }
     if (tid == 0) fb[i] = Cb;
+    DPI_BSTAMP(10);
     return;
   }
   const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
+  DPI_BSTAMP(5);
   int cur = 0;
   if (tid < H) dbuf[0][tid] = net.wout[tid] * act_d(net.act, act[L - 1][tid]);
   __syncthreads();
@@ -1514,6 +1576,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     cur ^= 1;
     __syncthreads();
   }
+  DPI_BSTAMP(6);
   float gs = 0.f, gA = 0.f, gB = 0.f;
   if (!Eq<KIND>::GRAD_FULL) {
     gs = block_sum_b(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
@@ -1528,6 +1591,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     gB = block_sum_b(B, red);
   }
   if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
+  DPI_BSTAMP(10);
 }
 
 struct PathArgs {

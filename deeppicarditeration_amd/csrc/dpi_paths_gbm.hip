@@ -11,3 +11,10 @@ extern "C" int dpi_debug_gbm_stamps(void* dst, size_t bytes) {
   return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(dpi::dpi_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 #endif
+
+#ifdef DPI_BASE_STAMPS
+// measurement variant (tools/base_stamps.py): the k_baseline phase stamps of this unit's launches
+extern "C" int dpi_debug_base_stamps_gbm(void* dst, size_t bytes) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(dpi::dpi_bstamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
