@@ -1411,7 +1411,12 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   // before the first FMA: one memory latency per layer); the slices are added in fixed order by
   // the unit's owner.
   __shared__ float part[NTHB];
+  [[maybe_unused]] int mv_n = 0;  // stamp variant: the second mat-vec's inner phases (events 11-13)
   auto matvec = [&](const float* __restrict__ Wt, const float* v, int K) -> float {
+#ifdef DPI_BASE_STAMPS
+    const bool mst = mv_n++ == 1;
+    if (mst) DPI_BSTAMP(11);
+#endif
     const int h = tid % H, ns = NTHB / H, sl = tid / H;
     const int kc = (K + ns - 1) / ns, k0 = sl * kc, k1 = min(K, k0 + kc);  // kc <= 16
     float w[16];
@@ -1424,10 +1429,22 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       if (k0 + j + 1 < k1) a1 = fmaf(w[j + 1], v[k0 + j + 1], a1);
     }
     part[tid] = a0 + a1;
+#ifdef DPI_BASE_STAMPS
+    if (mst) DPI_BSTAMP(12);
+#endif
     __syncthreads();
+#ifdef DPI_BASE_STAMPS
+    if (mst) DPI_BSTAMP(13);
+#endif
     float y = 0.f;
     if (tid < H)
       for (int j = 0; j < ns; ++j) y += part[j * H + tid];
+#ifdef DPI_BASE_STAMPS
+    if (mst) {
+      asm volatile("" ::"v"(y));  // (the stamp waits for y)
+      DPI_BSTAMP(14);
+    }
+#endif
     return y;  // valid for tid < H; the caller's barrier precedes the next use of part
   };
   // layer 1

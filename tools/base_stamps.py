@@ -5,7 +5,8 @@ Needs the stamp variant:
 then  DPI_HIP_LIB=tools/variants/libdpi_bstamps.so python tools/base_stamps.py
 Stamps (thread 0 of each block, after the barrier that closes a phase): 0 start, 1 point loaded /
 sampled, 2 g(x), 3 GBM exact-solution terms, 4 forward layers, 5 value (Cha) / adjoints (GBM),
-6 adjoint chain (Cha) / tangent init (GBM), 7-8 tangent layers (GBM), 10 end.  Prints the median
+6 adjoint chain (Cha) / tangent init (GBM), 7-8 tangent layers (GBM), 10 end; inside the second
+mat-vec: 11 start, 12 slice loads + fma done (part stored), 13 after its barrier, 14 owner sum done.  Prints the median
 cycles of each interval over the launch's blocks for the bench workloads' shapes."""
 import ctypes
 import sys
@@ -57,8 +58,10 @@ def main():
     ws = torch.empty(gen.workspace_bytes(n, 64), dtype=torch.uint8, device="cuda:0")
     for _ in range(20):
         gen.sample_points_baseline(n, 0, ws)
-    report("Burgers k_baseline<Cha> with in-block sampling (n = 1024)", read(lib, "cha"), min(n, NB),
-           [0, 1, 2, 4, 5, 6, 10])
+    st = read(lib, "cha")
+    report("Burgers k_baseline<Cha> with in-block sampling (n = 1024)", st, min(n, NB), [0, 1, 2, 4, 5, 6, 10])
+    report("  its second mat-vec (layer 2): loads + fma + part store / barrier / owner sum", st, min(n, NB),
+           [11, 12, 13, 14])
     tx, _ = gen.sample_t_and_x(n, point_base=0)
     for _ in range(20):
         gen.point_baseline(tx, ws=ws)
