@@ -10,7 +10,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("DPI_HIP_LIB", _HERE / "libdpi_hip.so"))
 
 # constants mirrored from include/dpi.h (checked against the header by tests/test_capi.py)
-DPI_ABI_VERSION = 3
+DPI_ABI_VERSION = 4
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
@@ -49,6 +49,7 @@ SIGNATURES = {
     "dpi_net_status_peek": (c_int, [c_void_p, c_int, P(c_int)]),
     "dpi_build_id": (c_int, [ctypes.c_char_p, c_size_t]),
     "dpi_workspace_bytes": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
+    "dpi_workspace_bytes_prepared": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_sample_points": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_void_p, c_void_p]),
     "dpi_sample_points_t": (c_int, [c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int, c_void_p,
                                     c_void_p]),
@@ -72,9 +73,10 @@ SIGNATURES = {
                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "dpi_workspace_bytes_hessians": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_label_moments_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
-                                           c_uint32, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
-    "dpi_label_finalize_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p,
-                                            c_size_t, c_void_p]),
+                                           c_uint32, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                                           c_void_p]),
+    "dpi_label_finalize_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p,
+                                            c_void_p, c_size_t, c_void_p]),
     "dpi_sums_reduce": (c_int, [c_void_p, c_int, c_size_t, c_void_p, c_void_p]),
     "dpi_generate_with_gradients_and_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64,
                                                          c_uint32, c_uint32, c_float, c_void_p, c_void_p, c_size_t,
@@ -129,7 +131,8 @@ def check_build_id(lib, path):
     want, got = B.source_hash(), build_id(lib)
     if got != want:
         raise DPIError(f"{path} was built from other sources (build id {got[:12]}, tree {want[:12]}): rebuild it with "
-                       "`python -m deeppicarditeration_amd.build` (hipcc --offload-arch=gfx950)")
+                       "`python -m deeppicarditeration_amd.build` (hipcc --offload-arch=gfx950; `--force` rebuilds every "
+                       "object)")
 
 
 def last_error(lib=None):

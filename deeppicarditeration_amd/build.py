@@ -3,9 +3,11 @@
 Thirteen translation units (the C-ABI / PIS / reduce TU, and per equation the k_paths family, its
 TD-estimator family and the Tanh-activation twins of both) compile in parallel to objects, then link into one
 shared library together with a generated one-function unit, `dpi_build_id()`, that returns the
-SHA-256 of the sources and flags (`source_hash`).  The same hash goes into `libdpi_hip.so.buildid`
-beside the library: a build is current when that file matches the tree's hash (not by mtime), and
-`_lib.load()` refuses a library whose embedded identity differs from the tree it is loaded from."""
+SHA-256 of the sources and flags (`source_hash`).  A build is current when the library itself
+embeds the tree's hash (not by mtime, and not by a side file that a checkout could leave behind
+next to a stale library), and `_lib.load()` refuses a library whose embedded identity differs from
+the tree it is loaded from.  `libdpi_hip.so.buildid` beside the library is an untracked copy of
+the hash for humans."""
 import hashlib
 import os
 import subprocess
@@ -45,10 +47,22 @@ def source_hash():
     return h.hexdigest()
 
 
+def embedded_id(lib=OUT):
+    """The build id compiled into `lib` (the 64-hex string of dpi_build_id), read from the file's
+    bytes without loading it; None if absent."""
+    import re
+    try:
+        data = Path(lib).read_bytes()
+    except OSError:
+        return None
+    hit = re.search(rb"(?<![0-9a-f])[0-9a-f]{64}(?![0-9a-f])", data)
+    return hit.group(0).decode() if hit else None
+
+
 def needs_build():
-    if not OUT.exists() or not BUILD_ID_FILE.exists():
+    if not OUT.exists():
         return True
-    return BUILD_ID_FILE.read_text().strip() != source_hash()
+    return source_hash().encode() not in OUT.read_bytes()
 
 
 def includes(path, seen=None):

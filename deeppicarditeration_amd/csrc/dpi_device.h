@@ -90,6 +90,11 @@ struct NetDev {
   // 2^s (max |2^s W| in [0.5, 1)), wus = 2^-s (pack_split_x3)
   const uint32_t* WU[4];     // (H, H)
   float wus[4];
+  // mlp_hdiag_split's operand scales (powers of two from the host's calibration pass,
+  // dpi_kernels.hip x3_exponent): hsa[l] = store scale of a_l as the forward B operand of layer l + 1,
+  // hsc[l] = wus[l] / hsa[l - 1]; tangent z'_l (the raw accumulator) = z_l / hzs[l], the operand of
+  // layer l + 1 = act'(a_l) hbs[l] z'_l
+  float hsa[4], hsc[4], hzs[4], hbs[4];
 };
 
 // ------------------------------------------------------------------------------ helpers
@@ -846,7 +851,6 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #endif
   constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
   constexpr int WXS = LdsGbm<H>::WXS;
-  constexpr float SA = 16.0f, SB = 64.0f;  // operand prescales: activations, tangents
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int jj = lane & 15, qq = lane >> 4;
   const int pp = 16 * wv + jj;
@@ -924,20 +928,20 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       act[0][T][r] = Act<ACT>::f(fmaf(cm, acc[r], fmaf(sh.vec[H + h], tau, sh.vec[h])));
     }
   }
-  // hidden layers: B = SA a_{l-1}, o = 2^s SA W a -> a_l = Act<ACT>::f(o wus / SA + b)
+  // hidden layers: B = SA a_{l-1} (SA = hsa[l - 1]), o = 2^s SA W a -> a_l = Act<ACT>::f(o wus / SA + b)
   {
-    float ones[HT][4];
-#pragma unroll
-    for (int T = 0; T < HT; ++T)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ones[T][r] = SA;
 #pragma unroll
     for (int l = 1; l < L; ++l) {
+      float ones[HT][4];
+#pragma unroll
+      for (int T = 0; T < HT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ones[T][r] = net.hsa[l - 1];
       half8 bh[NU], bl[NU];
       split_b(act[l - 1], ones, bh, bl);
       floatx4 o[HT];
       wmul(l, bh, bl, o);
-      const float sc = net.wus[l] * (1.0f / SA);
+      const float sc = net.hsc[l];
 #pragma unroll
       for (int T = 0; T < HT; ++T)
 #pragma unroll
@@ -974,14 +978,15 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       for (int r = 0; r < 4; ++r) lam[l][T][r] = fmaf(ac[r], SPLIT_INV, am[r]);
     }
   }
-  // per-unit constants of the sweep.  Tangent of layer l >= 1 is held as z'_l = (SB / wus_l) z_l
-  // (the raw accumulator); the next operand is SB elu'(a_l) z_l = (elu'(a_l) wus_l) z'_l, and
-  // lam_l elu''(a_l) z_l^2 = (lam_l elu''(a_l) (wus_l / SB)^2) z'_l^2.
+  // per-unit constants of the sweep.  Tangent of layer l >= 1 is held as z'_l = (SB_{l-1} / wus_l) z_l
+  // (the raw accumulator; SB_l = 2^eb[l], the tangent operand's store scale); the next operand is
+  // SB_l elu'(a_l) z_l = (elu'(a_l) wus_l SB_l / SB_{l-1}) z'_l = (elu'(a_l) hbs_l) z'_l, and
+  // lam_l elu''(a_l) z_l^2 = (lam_l elu''(a_l) hzs_l^2) z'_l^2, hzs_l = wus_l / SB_{l-1}.
   float fz[L > 1 ? L - 1 : 1][HT][4];
 #pragma unroll
   for (int l = 0; l < L; ++l) {
-    const float zs = l == 0 ? 1.0f : net.wus[l] * (1.0f / SB);
-    const float bs = l == 0 ? SB : net.wus[l];
+    const float zs = net.hzs[l];
+    const float bs = net.hbs[l];
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
@@ -1787,9 +1792,15 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
   floatx4 acc[9];
 #pragma unroll
   for (int sl = 0; sl < 9; ++sl) acc[sl] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // a.flags selects the estimators (workgroup-uniform): a call over n_estimate_terminal paths with
+  // DPI_TERMINAL and one over n_estimate_integral paths with DPI_INTEGRAL make the labels of unequal
+  // sample counts (data.py:845 vs :1164), each with its own identity part
+  const bool TERM = a.flags & DPI_TERMINAL, INTG = a.flags & DPI_INTEGRAL;
+  float aI = 0.f, aT = 0.f;
 
   // ---- integral term: N2 -> noise tile, w . N2 for the exact-solution terms
   __syncthreads();  // phase 3 is done with the integral noise tile
+  if (INTG) {
   {
     float fs[NSG];
 #pragma unroll
@@ -1829,10 +1840,12 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
   const float fbp = sh.fbp[pp];
   if (qq == 0) wgt[pp] = tmt * ((fplus + fminus - 2.f * fbp) * 0.5f / sh.smt[pp]);  // path pp, not this lane's
   __syncthreads();
-  const float aI = wgt[lane];  // lane = path
+  aI = wgt[lane];  // lane = path
   hess_accum<H, L>(sh, wgt, NT, acc);
+  }
 
   // ---- terminal term: N1 -> noise tile, g(x +- a sqrt(T-t) N1)
+  if (TERM) {
   __syncthreads();  // every wave is done reading N2 and the weights
   float gp[NSG], gm[NSG];
 #pragma unroll
@@ -1869,10 +1882,11 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
   };
   const float gplus = wave_stats(gp);
   const float gminus = wave_stats(gm);
-  const float aT = (gplus + gminus - 2.f * g_x) * 0.5f / tmt;
+  aT = (gplus + gminus - 2.f * g_x) * 0.5f / tmt;
   if (wv == 0) wgt[lane] = aT;
   __syncthreads();
   hess_accum<H, L>(sh, wgt, NT, acc);
+  }
 
   // ---- identity part
   const float dsum = wave_sum(aI + aT);

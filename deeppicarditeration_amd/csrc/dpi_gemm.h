@@ -151,7 +151,11 @@ namespace dpi {
 // accumulated into ONE fp32 accumulator (lo unscaled; relative error ~2^-22 where the residual is
 // an fp16 normal).  The weights are stored prescaled by a power of two 2^s (host, per matrix:
 // max |2^s W| in [0.5, 1)) so their residuals stay in fp16's normal range; the epilogue multiplies
-// by wscale = 2^-s (exact).
+// by wscale = 2^-s (exact).  The activations and cotangents are stored prescaled too, by a power
+// of two 2^e per operand and network (dpi_kernels.hip x3_exponent: rms ~4, so their residuals stay
+// normal whatever the network's scale): wscale also carries the input's 2^-e (and, for EPI_DELU,
+// the output's 2^e), EPI_BIAS_ELU multiplies its output by oscale = 2^e, and EPI_DELU reads the
+// saved activation as a 2^-e = ascale.
 //     OUT[m][n] = epi( wscale sum_k W'[n][k] X[m][k] ),  m = path (M rows), n = unit (Np, % 32), k (Kp, % 32)
 // W': (Np, Kp) packed split (Kp words per row); X rows at X + m ldx (Kp words); OUT / AUX rows at
 // + m ldc / + m ldaux (Np words).  MFMA A = W tile (rows n), B = X tile (columns m).
@@ -246,7 +250,8 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
                                         const uint32_t* __restrict__ W, float wscale, const float* __restrict__ X,
                                         int ldx, const float* __restrict__ X2, int ldx2, int nk1,
                                         float* __restrict__ OUT, int ldc, const float* __restrict__ bias,
-                                        const float* __restrict__ AUX, int ldaux, int stage_aux = 1) {
+                                        const float* __restrict__ AUX, int ldaux, float oscale, float ascale,
+                                        int stage_aux = 1) {
   static_assert(NT == 2 || NT == 4, "wave n-tiles");
   constexpr int BN = 32 * NT, BM = X3_BM, STAGE = (BN + BM) * 32, NWAVE = X3_THREADS / 64;
   constexpr int NINS = (BN + BM) / 8, PER_WAVE = NINS / NWAVE;  // DMA wave-instructions per chunk
@@ -473,7 +478,7 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
       if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
         if (EPI == EPI_BIAS_ELU)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+          for (int j = 0; j < 8; ++j) v[j] = (v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f) * oscale;
       } else {
         float a[8];
         if (AUXC && aux_lds) {
@@ -494,7 +499,7 @@ __device__ __forceinline__ void x3_tile(uint32_t* __restrict__ sm, int m0, int n
           x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
+        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : fmaf(a[j], ascale, 1.0f);
       }
       x3_put8(OUT + (size_t)m * ldc, 0, U, ql, v);
     }
@@ -519,7 +524,8 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3h(int M, int Kp, int 
                                                              const float* __restrict__ X2, int ldx2, int nk1,
                                                              float* __restrict__ OUT, int ldc,
                                                              const float* __restrict__ bias,
-                                                             const float* __restrict__ AUX, int ldaux) {
+                                                             const float* __restrict__ AUX, int ldaux, float oscale,
+                                                             float ascale) {
   constexpr int NT = 4, BN = 128, BM = X3H_BM, STAGE = X3HLds::STAGE, NWAVE = X3H_THREADS / 64;
   constexpr int PER_WAVE = (BN + BM) / 8 / NWAVE;  // 8 DMA wave-instructions per chunk
   typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -688,12 +694,12 @@ __global__ __launch_bounds__(X3H_THREADS, 2) void k_gemm_x3h(int M, int Kp, int 
       if (EPI == EPI_BIAS || EPI == EPI_BIAS_ELU) {
         if (EPI == EPI_BIAS_ELU)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+          for (int j = 0; j < 8; ++j) v[j] = (v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f) * oscale;
       } else {
         float a[8];
         x3_get8(AUX + (size_t)m * ldaux, 0, U, ql, a);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : a[j] + 1.0f;
+        for (int j = 0; j < 8; ++j) v[j] *= a[j] > 0.f ? 1.0f : fmaf(a[j], ascale, 1.0f);
       }
       x3_put8(OUT + (size_t)m * ldc, 0, U, ql, v);
     }
@@ -706,11 +712,12 @@ __global__ __launch_bounds__(X3_THREADS, 1) void k_gemm_x3(int M, int Kp, int n_
                                                            const float* __restrict__ X2, int ldx2, int nk1,
                                                            float* __restrict__ OUT, int ldc,
                                                            const float* __restrict__ bias,
-                                                           const float* __restrict__ AUX, int ldaux, int stage_aux) {
+                                                           const float* __restrict__ AUX, int ldaux, float oscale,
+                                                           float ascale, int stage_aux) {
   __shared__ X3Lds<NT> lds;
   const int tile = x3_tile_of_block(), mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
   x3_tile<EPI, NT, VAR>(lds.sm, mt * X3_BM, nt * 32 * NT, M, Kp, W, wscale, X, ldx, X2, ldx2, nk1, OUT, ldc, bias, AUX,
-                        ldaux, stage_aux);
+                        ldaux, oscale, ascale, stage_aux);
 }
 
 

@@ -308,6 +308,174 @@ static size_t pack_split(std::vector<float>& blob, int R, int C, F at) {
   return off;
 }
 
+// ---------------------------------------------------------------- operand exponents (split storage)
+// A value stored split with an unscaled residual, hi = fp16(v), lo = fp16(v - hi) (the x3 convention
+// of k_gemm_x3 / k_pis_net / k_pis_time and of the GBM tangent sweep), keeps fp32's relative precision
+// only while lo is an fp16 normal (|v| >~ 2^-2); below that its error is absolute, ~2^-25.  A network
+// with small weights makes every activation (or cotangent, or tangent) of a layer small, and the
+// products that read them then lose precision that exact fp32 keeps (tools/probe_small.py "homog").
+// So every such operand is stored as 2^e v, e per operand and network, chosen on the host from a
+// calibration pass of the network itself (double precision, fixed synthetic inputs) so that the
+// operand's rms is ~4: per element fp32-class down to ~rms/16, 2^14 of headroom above the rms before
+// fp16 overflows (the range guard's case).  The consuming product folds 2^-e into its weight scale,
+// so the arithmetic is a power of two per operand — exact.
+static int x3_exponent(double sumsq, double count) {
+  if (!(count > 0) || !(sumsq > 0) || !std::isfinite(sumsq)) return 0;
+  const int e = 2 - (int)std::lround(0.5 * std::log2(sumsq / count));
+  return std::min(std::max(e, -40), 40);
+}
+// fixed-seed N(0, 1) calibration inputs (splitmix64 + Box-Muller; host only, not a label draw)
+struct CalNormal {
+  uint64_t s = 0x9E3779B97F4A7C15ull;
+  double u01() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return ((double)((z ^ (z >> 31)) >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  }
+  double operator()() { return std::sqrt(-2.0 * std::log(u01())) * std::cos(6.283185307179586 * u01()); }
+};
+constexpr int CAL_ROWS = 16;
+static double cal_act(int act, double z) { return act == DPI_ACT_TANH ? std::tanh(z) : (z > 0 ? z : std::expm1(z)); }
+static double cal_dact(int act, double a) { return act == DPI_ACT_TANH ? 1.0 - a * a : (a > 0 ? 1.0 : a + 1.0); }
+// y = W x + b (W row-major (o, in)); b may be null
+static void cal_affine(const float* W, const float* b, int o, int in, const double* x, double* y) {
+  for (int r = 0; r < o; ++r) {
+    double a = b ? (double)b[r] : 0.0;
+    const float* w = W + (size_t)r * in;
+    for (int k = 0; k < in; ++k) a += (double)w[k] * x[k];
+    y[r] = a;
+  }
+}
+// y = W^T x (W row-major (o, in), x of length o)
+static void cal_affine_t(const float* W, int o, int in, const double* x, double* y) {
+  for (int k = 0; k < in; ++k) y[k] = 0.0;
+  for (int r = 0; r < o; ++r) {
+    const float* w = W + (size_t)r * in;
+    for (int k = 0; k < in; ++k) y[k] += (double)w[k] * x[r];
+  }
+}
+
+// PISGradNet's operand exponents: t_encoder's hidden layer (te) and output (temb), the operand of
+// smooth_net block j (sn[j]), nn_module's activations A_l (a[l]) and VJP cotangents D_l (d[l]).
+// Calibration rows: lambda evenly over (0, T), X ~ N(0, 4 I) (the OU/HJB state scale, x ~ N(0, (4 + t) I)).
+struct PisExps {
+  int te, temb, sn[4], a[4], d[4];
+};
+static PisExps pis_calibrate(int nx, int L, const int* hidden, double T, const float* phase, const float* coeff,
+                             const float* te0, const float* te0b, const float* te2, const float* te2b, const float* sn0,
+                             const float* sn0b, const float* const* snw, const float* const* snbw, int nsm,
+                             const float* const* nnw, const float* const* nnbw, const int* ins) {
+  const int C = PIS_CH;
+  double s_te = 0, s_temb = 0, s_sn[4] = {0, 0, 0, 0}, s_a[4] = {0, 0, 0, 0}, s_d[4] = {0, 0, 0, 0};
+  int hmax = C;
+  for (int l = 0; l < L; ++l) hmax = std::max(hmax, hidden[l]);
+  std::vector<double> e(2 * C), h(C), h2(C), in0(C + nx), A[4], D(hmax), D2(hmax);
+  for (int l = 0; l < L; ++l) A[l].assign(hidden[l], 0.0);
+  CalNormal nrm;
+  auto sq = [](const std::vector<double>& v, int n) {
+    double s = 0;
+    for (int k = 0; k < n; ++k) s += v[k] * v[k];
+    return s;
+  };
+  for (int r = 0; r < CAL_ROWS; ++r) {
+    const double lbd = T * (r + 0.5) / CAL_ROWS;
+    for (int j = 0; j < C; ++j) {
+      const double a = (double)coeff[j] * lbd + (double)phase[j];
+      e[j] = std::sin(a);
+      e[C + j] = std::cos(a);
+    }
+    cal_affine(te0, te0b, C, 2 * C, e.data(), h.data());
+    for (int k = 0; k < C; ++k) h[k] = cal_act(DPI_ACT_ELU, h[k]);
+    s_te += sq(h, C);
+    cal_affine(te2, te2b, C, C, h.data(), in0.data());
+    for (int k = 0; k < C; ++k) s_temb += in0[k] * in0[k];
+    cal_affine(sn0, sn0b, C, 2 * C, e.data(), h.data());
+    for (int j = 0; j < nsm; ++j) {
+      for (int k = 0; k < C; ++k) h[k] = cal_act(DPI_ACT_ELU, h[k]);
+      s_sn[j] += sq(h, C);
+      cal_affine(snw[j], snbw[j], C, C, h.data(), h2.data());
+      h.swap(h2);
+    }
+    for (int d = 0; d < nx; ++d) in0[C + d] = 2.0 * nrm();
+    const double* x = in0.data();
+    for (int l = 0; l < L; ++l) {
+      cal_affine(nnw[l], nnbw[l], hidden[l], ins[l], x, A[l].data());
+      for (int k = 0; k < hidden[l]; ++k) A[l][k] = cal_act(DPI_ACT_ELU, A[l][k]);
+      s_a[l] += sq(A[l], hidden[l]);
+      x = A[l].data();
+    }
+    // VJP with cotangent X on net_out: D_{L-1} = (nn_L^T X) elu'(A_{L-1}), D_{l-1} = (nn_l^T D_l) elu'(A_{l-1})
+    cal_affine_t(nnw[L], nx, ins[L], in0.data() + C, D.data());
+    for (int l = L - 1; l >= 0; --l) {
+      for (int k = 0; k < hidden[l]; ++k) D[k] *= cal_dact(DPI_ACT_ELU, A[l][k]);
+      s_d[l] += sq(D, hidden[l]);
+      if (l > 0) {
+        cal_affine_t(nnw[l], hidden[l], ins[l], D.data(), D2.data());
+        D.swap(D2);
+      }
+    }
+  }
+  PisExps x;
+  x.te = x3_exponent(s_te, (double)CAL_ROWS * C);
+  x.temb = x3_exponent(s_temb, (double)CAL_ROWS * C);
+  for (int j = 0; j < 4; ++j) x.sn[j] = j < nsm ? x3_exponent(s_sn[j], (double)CAL_ROWS * C) : 0;
+  for (int l = 0; l < 4; ++l) {
+    x.a[l] = l < L ? x3_exponent(s_a[l], (double)CAL_ROWS * hidden[l]) : 0;
+    x.d[l] = l < L ? x3_exponent(s_d[l], (double)CAL_ROWS * hidden[l]) : 0;
+  }
+  return x;
+}
+
+// The MLP tangent sweep's operand exponents (mlp_hdiag_split): activations a_l (the forward's B
+// operands of layers l + 1) and tangent operands act'(a_l) z_l, z_0 = W1x[:, d] over every direction d
+// (z_{l+1} = W_{l+1} (act'(a_l) z_l)).  Calibration rows: t evenly over (0, T), x ~ N(0, I).
+static void mlp_calibrate(int nx, int H, int L, int act, const float* W0, const float* b0, const float* const* W,
+                          const float* const* b, int* ea, int* eb) {
+  const int n_in = 1 + nx;
+  double sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  std::vector<double> x(n_in), a[4], z((size_t)H * nx), zn((size_t)H * nx);
+  for (int l = 0; l < L; ++l) a[l].assign(H, 0.0);
+  CalNormal nrm;
+  for (int r = 0; r < CAL_ROWS; ++r) {
+    x[0] = (r + 0.5) / CAL_ROWS;
+    for (int d = 0; d < nx; ++d) x[1 + d] = nrm();
+    cal_affine(W0, b0, H, n_in, x.data(), a[0].data());
+    for (int k = 0; k < H; ++k) a[0][k] = cal_act(act, a[0][k]);
+    for (int l = 1; l < L; ++l) {
+      cal_affine(W[l], b[l], H, H, a[l - 1].data(), a[l].data());
+      for (int k = 0; k < H; ++k) a[l][k] = cal_act(act, a[l][k]);
+    }
+    for (int l = 0; l + 1 < L; ++l)
+      for (int k = 0; k < H; ++k) sa[l] += a[l][k] * a[l][k];
+    if (r >= 4) continue;  // the tangents (H^2 nx per layer) from the first 4 rows
+    // tangents of every direction at once: z[h][d]
+    for (int h = 0; h < H; ++h)
+      for (int d = 0; d < nx; ++d) z[(size_t)h * nx + d] = W0[(size_t)h * n_in + 1 + d];
+    for (int l = 0; l + 1 < L; ++l) {
+      for (int h = 0; h < H; ++h) {
+        const double f = cal_dact(act, a[l][h]);
+        for (int d = 0; d < nx; ++d) {
+          z[(size_t)h * nx + d] *= f;
+          sb[l] += z[(size_t)h * nx + d] * z[(size_t)h * nx + d];
+        }
+      }
+      std::fill(zn.begin(), zn.end(), 0.0);
+      for (int o = 0; o < H; ++o)
+        for (int k = 0; k < H; ++k) {
+          const double w = W[l + 1][(size_t)o * H + k];
+          if (w != 0.0)
+            for (int d = 0; d < nx; ++d) zn[(size_t)o * nx + d] += w * z[(size_t)k * nx + d];
+        }
+      z.swap(zn);
+    }
+  }
+  for (int l = 0; l < 4; ++l) {
+    ea[l] = l + 1 < L ? x3_exponent(sa[l], (double)CAL_ROWS * H) : 0;
+    eb[l] = l + 1 < L ? x3_exponent(sb[l], 4.0 * H * nx) : 0;
+  }
+}
+
 extern "C" {
 
 int dpi_abi_version(void) { return DPI_ABI_VERSION; }
@@ -590,6 +758,7 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   const int nxp32 = (nx + 31) & ~31;
   size_t oW1xS = 0, oW1xTS = 0, oWS[4] = {0}, oWTS[4] = {0}, oWU[4] = {0};
   float wus[4] = {1.f, 1.f, 1.f, 1.f};
+  int ea[4] = {0, 0, 0, 0}, eb[4] = {0, 0, 0, 0};  // mlp_hdiag_split's operand exponents
   if (H % 32 == 0) {
     auto Wx = [&](int h, int d) { return d < nx ? W0[(size_t)h * n_in + 1 + d] : 0.f; };
     oW1xS = pack_split(blob, H, nxp32, Wx);
@@ -601,6 +770,9 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
       oWTS[l] = pack_split(blob, H, H, [&](int r, int c) { return Wc[(size_t)c * H + r]; });
       oWU[l] = pack_split_x3(blob, H, H, [&](int r, int c) { return Wc[(size_t)r * H + c]; }, &wus[l]);
     }
+    const float *Wl[4] = {nullptr, nullptr, nullptr, nullptr}, *bl[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int l = 1; l < L; ++l) Wl[l] = blob.data() + oW[l], bl[l] = blob.data() + ob[l];
+    mlp_calibrate(nx, H, L, act, W0, b0, Wl, bl, ea, eb);
   }
   auto* n = new dpi_net_s();
   std::memset(&n->d, 0, sizeof(n->d));
@@ -644,6 +816,13 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
       n->d.WTS[l] = u32(oWTS[l]);
       n->d.WU[l] = u32(oWU[l]);
       n->d.wus[l] = wus[l];
+    }
+    // mlp_hdiag_split: forward operand of layer l + 1 = 2^ea[l] a_l, tangent operand = 2^eb[l] act'(a_l) z_l
+    for (int l = 0; l < L; ++l) {
+      n->d.hsa[l] = std::ldexp(1.0f, ea[l]);
+      if (l >= 1) n->d.hsc[l] = std::ldexp(wus[l], -ea[l - 1]);
+      n->d.hzs[l] = l == 0 ? 1.0f : std::ldexp(wus[l], -eb[l - 1]);
+      n->d.hbs[l] = l == 0 ? std::ldexp(1.0f, eb[0]) : std::ldexp(wus[l], eb[l] - eb[l - 1]);
     }
   }
   if (int rc = net_init_status(n, given, n_params)) {
@@ -744,6 +923,8 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
     for (int k = 0; k < C; ++k) a += (double)snl[k] * elu_d(h[k]);
     smooth0 = a;
   }
+  const PisExps ex =
+      pis_calibrate(nx, L, hidden, T, phase, coeff, te0, te0b, te2, te2b, sn0, sn0b, snw, snbw, nsm, nnw, nnbw, ins);
   NetPisDev pd;
   std::memset(&pd, 0, sizeof(pd));
   size_t o_phase = put(phase, C), o_coeff = put(coeff, C), o_te0 = put(te0, (size_t)C * 2 * C), o_te0b = put(te0b, C),
@@ -778,17 +959,40 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
         return (r < rows && c < cols) ? src[(size_t)r * cols + c] : 0.f;
       }, ws);
     };
+    // every product's weight scale carries its stored input's 2^-e (x3_exponent); the VJP's also
+    // its output's 2^e (EPI_DELU stores (acc ws) elu'(A))
     s_te0 = packm(te0, C, 2 * C, C, 2 * C, false, &w_te0);
     s_te2 = packm(te2, C, C, C, C, false, &w_te2);
+    w_te2 = std::ldexp(w_te2, -ex.te);
     s_sn0 = packm(sn0, C, 2 * C, C, 2 * C, false, &w_sn0);
-    for (int j = 0; j < nsm; ++j) s_sn[j] = packm(snw[j], C, C, C, C, false, &w_sn[j]);
-    // forward: nn[0] (h0 x (64 + nx)), nn[l] (h_l x h_{l-1}), nn[L] (nx x h_{L-1})
-    s_nn[0] = packm(nnw[0], hidden[0], ins[0], hp[0], INP, false, &w_nn[0]);
-    for (int l = 1; l < L; ++l) s_nn[l] = packm(nnw[l], hidden[l], ins[l], hp[l], hp[l - 1], false, &w_nn[l]);
+    for (int j = 0; j < nsm; ++j) {
+      s_sn[j] = packm(snw[j], C, C, C, C, false, &w_sn[j]);
+      w_sn[j] = std::ldexp(w_sn[j], -ex.sn[j]);
+    }
+    // forward: nn[0] (h0 x (64 + nx)), nn[l] (h_l x h_{l-1}), nn[L] (nx x h_{L-1}); nn[0]'s t_emb
+    // columns carry t_emb's 2^-e (IN holds [2^e t_emb | X], two operands in one K)
+    {
+      align();
+      const float* w0 = nnw[0];
+      const int in0 = ins[0], h0 = hidden[0];
+      s_nn[0] = pack_split_x3(blob, hp[0], INP, [&](int r, int c) {
+        if (r >= h0 || c >= in0) return 0.f;
+        return c < C ? std::ldexp(w0[(size_t)r * in0 + c], -ex.temb) : w0[(size_t)r * in0 + c];
+      }, &w_nn[0]);
+    }
+    for (int l = 1; l < L; ++l) {
+      s_nn[l] = packm(nnw[l], hidden[l], ins[l], hp[l], hp[l - 1], false, &w_nn[l]);
+      w_nn[l] = std::ldexp(w_nn[l], -ex.a[l - 1]);
+    }
     s_nn[L] = packm(nnw[L], nx, ins[L], NOP, hp[L - 1], false, &w_nn[L]);
+    w_nn[L] = std::ldexp(w_nn[L], -ex.a[L - 1]);
     // VJP: nnT[L] = nn[L]^T (h_{L-1} x nx), nnT[l] = nn[l]^T, nnT[0] = nn[0][:, 64:]^T (nx x h0)
     s_nnT[L] = packm(nnw[L], nx, ins[L], hp[L - 1], NXK, true, &w_nnT[L]);
-    for (int l = 1; l < L; ++l) s_nnT[l] = packm(nnw[l], hidden[l], ins[l], hp[l - 1], hp[l], true, &w_nnT[l]);
+    w_nnT[L] = std::ldexp(w_nnT[L], ex.d[L - 1]);
+    for (int l = 1; l < L; ++l) {
+      s_nnT[l] = packm(nnw[l], hidden[l], ins[l], hp[l - 1], hp[l], true, &w_nnT[l]);
+      w_nnT[l] = std::ldexp(w_nnT[l], ex.d[l - 1] - ex.d[l]);
+    }
     {
       align();
       const float* w0 = nnw[0];
@@ -802,11 +1006,12 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
       const float *w0 = nnw[0], *wl = nnw[L];
       const int in0 = ins[0], h0 = hidden[0], inl = ins[L];
       // K order [A_{L-1} | D_0]: k_pis_net forms the A_{L-1} half while A_{L-1} is still in LDS
+      // (the two halves' columns carry 2^-e of A_{L-1} resp. D_0)
       s_gxno = pack_split_x3(blob, NOP, hp[L - 1] + hp[0], [&](int d, int k) {
         if (d >= nx) return 0.f;
-        if (k < hp[L - 1]) return k < inl ? wl[(size_t)d * inl + k] : 0.f;
+        if (k < hp[L - 1]) return k < inl ? std::ldexp(wl[(size_t)d * inl + k], -ex.a[L - 1]) : 0.f;
         k -= hp[L - 1];
-        return k < h0 ? w0[(size_t)k * in0 + C + d] : 0.f;
+        return k < h0 ? std::ldexp(w0[(size_t)k * in0 + C + d], -ex.d[0]) : 0.f;
       }, &w_gxno);
     }
     for (int l = 0; l <= L; ++l) {
@@ -867,6 +1072,13 @@ int dpi_net_create_pisgrad(int nx, int n_hidden, const int* hidden, double T, co
     pd.gxnoS = u32(s_gxno);
     pd.gxnoF = u32(s_gxnoF);
     pd.gxnoW = w_gxno;
+    pd.xs_te = std::ldexp(1.0f, ex.te);
+    pd.xs_temb = std::ldexp(1.0f, ex.temb);
+    for (int j = 0; j < 4; ++j) pd.xs_sn[j] = std::ldexp(1.0f, ex.sn[j]);
+    for (int l = 0; l < 4; ++l) {
+      pd.nnO[l] = std::ldexp(1.0f, ex.a[l]);
+      pd.nnA[l] = std::ldexp(1.0f, -ex.a[l]);
+    }
     for (int l = 0; l <= L; ++l) {
       pd.nnS[l] = u32(s_nn[l]);
       pd.nnTS[l] = u32(s_nnT[l]);
@@ -1077,7 +1289,7 @@ static int x3_tile_rows() {
 template <int NT>
 static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx,
                        const float* X2, int ldx2, int k1, float* OUT, int ldc, const float* bias, const float* aux,
-                       int ldaux, hipStream_t st) {
+                       int ldaux, float os, float as, hipStream_t st) {
   const int nnt = Np / (32 * NT), nmt = (M + X3_BM - 1) / X3_BM, nk1 = k1 / 32;
   if constexpr (NT == 4) {
     if (x3_tile_rows() == 128) {
@@ -1085,36 +1297,38 @@ static void gemm_x3_nt(int epi, int M, int Kp, int Np, const uint32_t* W, float 
       dim3 gh(nnt * nmh), bh(X3H_THREADS);
       if (epi == EPI_BIAS)
         hipLaunchKernelGGL(k_gemm_x3h<EPI_BIAS>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc, bias,
-                           aux, ldaux);
+                           aux, ldaux, os, as);
       else if (epi == EPI_BIAS_ELU)
         hipLaunchKernelGGL(k_gemm_x3h<EPI_BIAS_ELU>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc,
-                           bias, aux, ldaux);
+                           bias, aux, ldaux, os, as);
       else
         hipLaunchKernelGGL(k_gemm_x3h<EPI_DELU>, gh, bh, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT, ldc, bias,
-                           aux, ldaux);
+                           aux, ldaux, os, as);
       return;
     }
   }
   dim3 grid(nnt * nmt), block(X3_THREADS);
   if (epi == EPI_BIAS)
     hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
-                       ldc, bias, aux, ldaux, 0);
+                       ldc, bias, aux, ldaux, os, as, 0);
   else if (epi == EPI_BIAS_ELU)
     hipLaunchKernelGGL((k_gemm_x3<EPI_BIAS_ELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1,
-                       OUT, ldc, bias, aux, ldaux, 0);
+                       OUT, ldc, bias, aux, ldaux, os, as, 0);
   else
     hipLaunchKernelGGL((k_gemm_x3<EPI_DELU, NT>), grid, block, 0, st, M, Kp, nnt, W, ws, X, ldx, X2, ldx2, nk1, OUT,
-                       ldc, bias, aux, ldaux, x3_stage_aux());
+                       ldc, bias, aux, ldaux, os, as, x3_stage_aux());
 }
-// ws: the weight matrix's scale 2^-s (pack_split_x3).  X2 != nullptr: K columns [k1, Kp) come from X2.
+// ws: the weight matrix's scale 2^-s (pack_split_x3) with the operand exponents folded in; os / as:
+// the ELU output's store scale / the DELU operand's read scale (dpi_gemm.h).  X2 != nullptr: K
+// columns [k1, Kp) come from X2.
 static void gemm_x3(int epi, int M, int Kp, int Np, const uint32_t* W, float ws, const float* X, int ldx, float* OUT,
-                    int ldc, const float* bias, const float* aux, int ldaux, hipStream_t st,
+                    int ldc, const float* bias, const float* aux, int ldaux, float os, float as, hipStream_t st,
                     const float* X2 = nullptr, int ldx2 = 0, int k1 = 0) {  // Np % 64 == 0, Kp % 32 == 0
   if (!X2) X2 = X, ldx2 = ldx, k1 = Kp;
   if (Np % 128 == 0)
-    gemm_x3_nt<4>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<4>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, os, as, st);
   else
-    gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, st);
+    gemm_x3_nt<2>(epi, M, Kp, Np, W, ws, X, ldx, X2, ldx2, k1, OUT, ldc, bias, aux, ldaux, os, as, st);
 }
 
 // k_pis_net (the fused split VJP chain) by default; DPI_PIS_FUSED=0 selects the layer-wise
@@ -1173,12 +1387,14 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   const float* a = rows + L.IN;
   for (int l = 0; l < pd.L; ++l) {
     const int Np = r64(pd.h[l]);
-    gemm_x3(EPI_BIAS_ELU, R, Kp, Np, pd.nnS[l], pd.nnW[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, st);
+    gemm_x3(EPI_BIAS_ELU, R, Kp, Np, pd.nnS[l], pd.nnW[l], a, ld, rows + L.A[l], ld, pd.nnbP[l], nullptr, 0, pd.nnO[l],
+            1.0f, st);
     a = rows + L.A[l];
     Kp = Np;
   }
   if (!vjp) {  // forward only (TD terminal value): net_out
-    gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, st);
+    gemm_x3(EPI_BIAS, R, Kp, NOP, pd.nnS[pd.L], pd.nnW[pd.L], a, ld, rows + L.NO, ld, pd.nnbP[pd.L], nullptr, 0, 1.0f, 1.0f,
+            st);
     return L;
   }
   // VJP: the x part of IN starts at its chunk 2 (word 64).  (Fusing this product into the last
@@ -1186,16 +1402,16 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
   // faster: 828 us against 487 + 335 us.)
   int dcur = L.D0, dnext = L.D1;
   gemm_x3(EPI_DELU, R, NXK, r64(pd.h[pd.L - 1]), pd.nnTS[pd.L], pd.nnTW[pd.L], rows + L.IN + 2 * 32, ld, rows + dcur, ld,
-          nullptr, rows + L.A[pd.L - 1], ld, st);
+          nullptr, rows + L.A[pd.L - 1], ld, 1.0f, pd.nnA[pd.L - 1], st);
   for (int l = pd.L - 1; l >= 1; --l) {
     gemm_x3(EPI_DELU, R, r64(pd.h[l]), r64(pd.h[l - 1]), pd.nnTS[l], pd.nnTW[l], rows + dcur, ld, rows + dnext, ld, nullptr,
-            rows + L.A[l - 1], ld, st);
+            rows + L.A[l - 1], ld, 1.0f, pd.nnA[l - 1], st);
     std::swap(dcur, dnext);
   }
   // GX = net_out + J^T X = [A_{L-1} | D_0] . [nn[L] | nnT[0]]^T + b_L: one GEMM with K = h_{L-1} + h_0,
   // the A_{L-1} chunks first (k_pis_net's order; k_pis_final and k_pis_base_final only need the sum)
   gemm_x3(EPI_BIAS, R, Kp + r64(pd.h[0]), NOP, pd.gxnoS, pd.gxnoW, rows + L.A[pd.L - 1], ld, rows + L.GX, ld,
-          pd.nnbP[pd.L], nullptr, 0, st, rows + dcur, ld, Kp);
+          pd.nnbP[pd.L], nullptr, 0, 1.0f, 1.0f, st, rows + dcur, ld, Kp);
   return L;
 }
 
@@ -1240,6 +1456,12 @@ static PisRows pis_chain(const NetPisDev& pd, float* rows, int R, hipStream_t st
 }
 
 extern "C" size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M) {
+  if (!p || n < 0 || M < 0) return 0;
+  return ws_layout(net, n, M, 1 + p->e.nx).total;
+}
+// + the staged noise sums of a GBM MLP net's prepared calls (the last region of the layout, so a
+// plain call's offsets are the same)
+extern "C" size_t dpi_workspace_bytes_prepared(dpi_problem p, dpi_net net, int n, int M) {
   if (!p || n < 0 || M < 0) return 0;
   return ws_layout(net, n, M, 1 + p->e.nx, gbm_noise_prep(p, net)).total;
 }
@@ -1534,6 +1756,7 @@ static int path_order() {
 static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                       uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, bool need_moments,
                       const float* moments, void* ws, size_t ws_bytes, WsLayout* w, PathArgs* pa) {
+  const bool prepared = !need_moments || (flags & DPI_PREPARED);  // dpi_label_prepare, or its prepared call
   int rc = check_pair(p, net);
   if (rc) return rc;
   if (n < 0 || (n && (!tx || !ws || (need_moments && !moments))) || K < 1 || M < 1 || m_begin < 0 || m_end > M ||
@@ -1544,8 +1767,11 @@ static int label_args(dpi_problem p, dpi_net net, const float* tx, int n, int M,
   const int F = 1 + p->e.nx;
   const int nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "label_moments: at most DPI_PATHS_PER_CALL_MAX paths per call");
-  *w = ws_layout(net, n, M, F, gbm_noise_prep(p, net));
-  if (ws_bytes < w->total) return fail(DPI_ERR_WORKSPACE, "workspace too small");
+  // the noise staging region only for dpi_label_prepare and the DPI_PREPARED call it feeds
+  *w = ws_layout(net, n, M, F, prepared && gbm_noise_prep(p, net));
+  if (ws_bytes < w->total)
+    return fail(DPI_ERR_WORKSPACE, prepared ? "workspace too small (prepared calls: dpi_workspace_bytes_prepared)"
+                                            : "workspace too small");
   char* b = (char*)ws;
   PathArgs& a = *pa;
   std::memset(&a, 0, sizeof(a));
@@ -1851,16 +2077,17 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M) {
 }
 
 static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
-                             uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments, float* hsum,
-                             void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
+                             uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
+                             float* hsum, void* ws, size_t ws_bytes, void* stream, float* y, float bound) {
   int rc = check_pair(p, net);
   if (rc) return rc;
   if (p->e.kind != DPI_EQ_GBM)
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
   if (net->d.kind == 2) return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: MLP or ZeroSolution networks only");
   if (n < 0 || (n && (!tx || !ws || !moments)) || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
-      (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu)
-    return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1)");
+      (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu || !(flags & DPI_BOTH) || (flags & ~DPI_BOTH))
+    return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1, flags in "
+                             "DPI_TERMINAL | DPI_INTEGRAL)");
   if (n == 0) return 0;
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "Hessian labels: at most DPI_PATHS_PER_CALL_MAX paths per call");
@@ -1881,7 +2108,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.nbp = nbp;
   a.m_begin = m_begin;
   a.K = K;
-  a.flags = DPI_BOTH;
+  a.flags = flags;
   a.k0 = (uint32_t)seed;
   a.k1 = (uint32_t)(seed >> 32);
   a.c3t = DPI_TAG_TERM | (epoch << 8);
@@ -1901,7 +2128,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_reduce, dim3(n, (2 * F + 3) / 4), dim3(256), 0, st, a.partial, n, F, nbp, moments, a.gx,
-                     1.0f / (float)M, 1, bound, y, F + C, net_status(net));
+                     1.0f / (float)M, (flags & DPI_TERMINAL) ? 1 : 0, bound, y, F + C, net_status(net));
   const int bpp = hess_tiles(nx);  // 256 packed words per workgroup: one 16 x 16 tile
   hipLaunchKernelGGL(k_reduce_hess, dim3((unsigned)((n + 7) / 8) * 8 * bpp), dim3(256), 0, st, a.hpart, n, nx, NT, nbp,
                      bpp, hsum, 1.0f / (float)M, bound, y, F + C, F, net_status(net));
@@ -1910,16 +2137,17 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
 }
 
 int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
-                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments,
+                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                                float* hessian_sums, void* ws, size_t ws_bytes, void* stream) {
   if (!hessian_sums) return fail(DPI_ERR_ARG, "label_moments_hessians: null hessian_sums");
-  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, moments, hessian_sums, ws,
-                           ws_bytes, stream, nullptr, 0.f);
+  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, moments, hessian_sums,
+                           ws, ws_bytes, stream, nullptr, 0.f);
 }
 
-int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M,
+int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M, int flags,
                                 float sample_bound, float* y, void* ws, size_t ws_bytes, void* stream) {
-  if (!p || n < 0 || (n && (!moments || !hessian_sums || !y || !ws)) || M < 1)
+  if (!p || n < 0 || (n && (!moments || !hessian_sums || !y || !ws)) || M < 1 || !(flags & DPI_BOTH) ||
+      (flags & ~DPI_BOTH))
     return fail(DPI_ERR_ARG, "label_finalize_hessians: bad arguments");
   if (n == 0) return 0;
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx;
@@ -1927,7 +2155,7 @@ int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float
   hipStream_t st = (hipStream_t)stream;
   const float* gx = (const float*)ws;  // WsLayout: gx at offset 0 (written by dpi_point_baseline)
   hipLaunchKernelGGL(k_finalize_y, dim3((n * F + 255) / 256), dim3(256), 0, st, moments, gx, n, F, 1.0f / (float)M,
-                     1, sample_bound, y, F + C);
+                     (flags & DPI_TERMINAL) ? 1 : 0, sample_bound, y, F + C);
   const size_t tot = (size_t)n * C;
   hipLaunchKernelGGL(k_finalize_hess, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, hessian_sums, n, C,
                      1.0f / (float)M, sample_bound, y, F + C, F);
@@ -1950,8 +2178,8 @@ int dpi_generate_with_gradients_and_hessians(dpi_problem p, dpi_net net, const f
   size_t moff;
   hess_extra(n, M, p->e.nx, &moff);
   float* moments = (float*)((char*)ws + al256(w.total) + moff);
-  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, moments, nullptr, ws, ws_bytes, stream,
-                           y, sample_bound);
+  return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, DPI_BOTH, moments, nullptr, ws, ws_bytes,
+                           stream, y, sample_bound);
 }
 
 }  // extern "C"

@@ -49,8 +49,14 @@ struct NetPisDev {
   // 2 KB block, the 64 lanes' hi granules (lane l: row 16 T + l % 16, granule pair l / 16) then
   // their lo granules, so each weight-fragment load is one contiguous 1 KB (8 whole lines)
   const uint32_t *nnF[5], *nnTF[5], *gxnoF;
-  // k_gemm_x3 weight scales 2^-s (each split matrix is stored prescaled by 2^s)
+  // k_gemm_x3 weight scales 2^-s (each split matrix is stored prescaled by 2^s), times the operand
+  // exponents of the stored inputs (2^-e) and, for the VJP products, of the output (2^e)
   float te0W, te2W, sn0W, snW[4], nnW[5], nnTW[5], gxnoW;
+  // operand exponents (dpi_kernels.hip x3_exponent): the store scale 2^e of every split operand the
+  // network's products read — k_pis_time's t_encoder hidden layer (xs_te), its output, IN[:, 0:64]
+  // (xs_temb), the operand of smooth_net block j (xs_sn[j]); nn_module's A_l (nnO[l]; read back by
+  // elu' as nnA[l] = 2^-e).  X (IN[:, 64:]) and GX / NO are stored unscaled.
+  float xs_te, xs_temb, xs_sn[4], nnO[4], nnA[4];
 };
 
 __device__ __forceinline__ void pis_embed(const NetPisDev& pn, float lbd, float* out /* stride 1 */, int j) {
@@ -415,13 +421,14 @@ __global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float*
       lo[j] = (_Float16)(v[j] - (float)h);
     }
   };
-  // activations (C layout, unit 16 T + 4 qq + r) -> B chunks u = 0, 1 (units 32 u + 4 qq + (j & 3) + 16 (j >> 2))
-  auto to_b = [&](const float (&a)[4][4], h8 (&bh)[2], h8 (&bl)[2]) {
+  // activations (C layout, unit 16 T + 4 qq + r) x the operand's store scale xs -> B chunks u = 0, 1
+  // (units 32 u + 4 qq + (j & 3) + 16 (j >> 2))
+  auto to_b = [&](const float (&a)[4][4], float xs, h8 (&bh)[2], h8 (&bl)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3];
+      for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3] * xs;
       split(v, bh[u], bl[u]);
     }
   };
@@ -462,7 +469,7 @@ __global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float*
     // t_encoder: Linear(128, 64), ELU, Linear(64, 64) -> IN[:, 0:64]
     layer(0, std::integral_constant<int, 4>{}, eh, el, acc);
     epi(acc, pn.te0W, pn.te0b, true, a);
-    to_b(a, bh, bl);
+    to_b(a, pn.xs_te, bh, bl);
     layer(2 * W2, std::integral_constant<int, 2>{}, bh, bl, acc);
     epi(acc, pn.te2W, pn.te2b, false, a);
     if (16 * tile + jj < R) {
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float*
       for (int u = 0; u < 2; ++u) {
         float v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3];
+        for (int j = 0; j < 8; ++j) v[j] = a[2 * u + (j >> 2)][j & 3] * pn.xs_temb;
         x3_put8(row, L.IN, u, qq, v);
       }
     }
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(PT_THREADS, 1) void k_pis_time(NetPisDev pn, float*
     layer(W2, std::integral_constant<int, 4>{}, eh, el, acc);
     epi(acc, pn.sn0W, pn.sn0b, true, a);
     for (int j = 0; j < nsm; ++j) {
-      to_b(a, bh, bl);
+      to_b(a, pn.xs_sn[j], bh, bl);
       layer(2 * W2 + (1 + j) * W1, std::integral_constant<int, 2>{}, bh, bl, acc);
       epi(acc, pn.snW[j], pn.snb[j], true, a);
     }

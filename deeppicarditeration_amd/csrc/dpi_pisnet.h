@@ -281,8 +281,10 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     const int m = 16 * b + il;
     return reinterpret_cast<u32x4_t*>(act(2 * wv + c) + m * 32 + 4 * ((2 * ql + hl) ^ x3_swz(m)));
   };
-  auto epilogue = [&](int kind, float ws, const float* bias, int save_reg, const u32x4_t (&xh)[4][2],
-                      const u32x4_t (&xl)[4][2]) {
+  // os: the output's store scale 2^e (PN_ELU), as: the saved activation's read scale 2^-e (PN_DELU_*),
+  // the operand exponents of dpi_gemm.h (k_gemm_x3h's oscale / ascale)
+  auto epilogue = [&](int kind, float ws, const float* bias, int save_reg, float os, float as,
+                      const u32x4_t (&xh)[4][2], const u32x4_t (&xl)[4][2]) {
     const __amdgpu_buffer_rsrc_t rb = pn_rsrc(bias, 4 * PN_H);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
             v[4 + r] = __builtin_fmaf(acc[2 * c + 1][b][r], ws, b1[r]);
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f;
+          for (int j = 0; j < 8; ++j) v[j] = (v[j] > 0.f ? v[j] : __expf(v[j]) - 1.0f) * os;
         } else {  // EPI_DELU: (acc 2^-s) elu'(A)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float a = x3_join(ah[j >> 1], al[j >> 1], j & 1);
-            v[j] *= a > 0.f ? 1.0f : a + 1.0f;
+            v[j] *= a > 0.f ? 1.0f : fmaf(a, as, 1.0f);
           }
         }
         u32x4_t eh, el;
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
       pre_vjp(NL);
     pn_barrier();  // every wave's reads of the layer input are done
     // A_{L-1} stays in LDS only: GX's A_{L-1} half is formed below and elu'(A_{L-1}) read from the image
-    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], l + 1 < NL ? L.A[l] : -1, xh, xl);
+    epilogue(PN_ELU, pd.nnW[l], pd.nnbP[l], l + 1 < NL ? L.A[l] : -1, pd.nnO[l], 1.0f, xh, xl);
     pn_barrier();
   }
   // VJP: D_{L-1} from X (xs) and elu'(A_{L-1}) (act: each wave reads and overwrites only its own
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
 #pragma unroll
       for (int b = 0; b < 4; ++b)
         *reinterpret_cast<pn_f4*>(gxs + (16 * b + il) * 128 + 16 * wv + 4 * ql) = ag[0][b];
-    epilogue(PN_DELU_LDS, pd.nnTW[NL], nullptr, -1, xh, xl);
+    epilogue(PN_DELU_LDS, pd.nnTW[NL], nullptr, -1, 1.0f, pd.nnA[NL - 1], xh, xl);
     pn_barrier();
   }
 #pragma unroll
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(PN_THREADS, 1) __attribute__((amdgpu_num_vgpr(DPI_P
     else
       pre_gx(PN_HC);
     pn_barrier();
-    epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, xh, xl);
+    epilogue(PN_DELU_HBM, pd.nnTW[l], nullptr, -1, 1.0f, pd.nnA[l - 1], xh, xl);
     pn_barrier();
   }
   // GX = [A_{L-1} | D_0] . gxno^T + b_L (K = 1,024): the A_{L-1} half's partial sums back from the

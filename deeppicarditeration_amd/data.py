@@ -540,8 +540,11 @@ class OnlineDataGenerator:
         return self._dataset(n_total, n_batch_buffer, batch_size, self.sample_exact_with_gradients_and_hessians, guard=False)
 
     # ------------------------------------------------------------------ moments (sharding building blocks)
-    def workspace_bytes(self, n, M, hessians=False):
-        need = self.lib.dpi_workspace_bytes(self.problem, self.net.handle, n, M)
+    def workspace_bytes(self, n, M, hessians=False, prepared=False):
+        """Device workspace (bytes) of n points x M paths; prepared: for label_prepare and the
+        DPI_PREPARED label_moments call it feeds (include/dpi.h dpi_workspace_bytes_prepared)."""
+        fn = self.lib.dpi_workspace_bytes_prepared if prepared else self.lib.dpi_workspace_bytes
+        need = fn(self.problem, self.net.handle, n, M)
         if hessians:
             need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
         return need
@@ -615,32 +618,33 @@ class OnlineDataGenerator:
                                                ws.numel(), _stream(self._device)), "dpi_label_finalize")
         return y
 
-    def label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
-        """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2).
-        More than PATHS_PER_CALL_MAX paths run as several calls combined by sums_reduce."""
+    def label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws, flags=_lib.DPI_BOTH):
+        """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2),
+        of the estimators `flags` selects (DPI_TERMINAL / DPI_INTEGRAL / both).  More than
+        PATHS_PER_CALL_MAX paths run as several calls combined by sums_reduce."""
         pieces = self._pieces(m_begin, m_end)
         if len(pieces) > 1:
-            parts = [self._label_moments_hessians(tx, point_base, M, a, b, ws) for a, b in pieces]
+            parts = [self._label_moments_hessians(tx, point_base, M, a, b, ws, flags) for a, b in pieces]
             return (self.sums_reduce(torch.stack([p[0] for p in parts])),
                     self.sums_reduce(torch.stack([p[1] for p in parts])))
-        return self._label_moments_hessians(tx, point_base, M, m_begin, m_end, ws)
+        return self._label_moments_hessians(tx, point_base, M, m_begin, m_end, ws, flags)
 
-    def _label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws):
+    def _label_moments_hessians(self, tx, point_base, M, m_begin, m_end, ws, flags=_lib.DPI_BOTH):
         n, nx = tx.shape[0], self.equation.nx
         mom = torch.empty(n, 2, 1 + nx, dtype=torch.float32, device=self._device)
         hs = torch.empty(n, nx * nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
         _lib.check(self.lib.dpi_label_moments_hessians(
             self.problem, self.net.handle, _ptr(tx), n, M, self.K, self.seed, self.epoch, point_base, m_begin, m_end,
-            _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self._device)), "dpi_label_moments_hessians")
+            flags, _ptr(mom), _ptr(hs), _ptr(ws), ws.numel(), _stream(self._device)), "dpi_label_moments_hessians")
         return mom, hs
 
-    def finalize_hessians(self, moments, hsums, M, ws, bound=None):
+    def finalize_hessians(self, moments, hsums, M, ws, bound=None, flags=_lib.DPI_BOTH):
         n, nx = moments.shape[0], self.equation.nx
         y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self._device)
         b = self.sample_bound if bound is None else bound
-        _lib.check(self.lib.dpi_label_finalize_hessians(self.problem, _ptr(moments), _ptr(hsums), n, M, b, _ptr(y),
-                                                        _ptr(ws), ws.numel(), _stream(self._device)),
+        _lib.check(self.lib.dpi_label_finalize_hessians(self.problem, _ptr(moments), _ptr(hsums), n, M, flags, b,
+                                                        _ptr(y), _ptr(ws), ws.numel(), _stream(self._device)),
                    "dpi_label_finalize_hessians")
         return y
 
@@ -710,8 +714,14 @@ class OnlineDataGenerator:
         return self._guarded(lambda: self._generate_hess_once(tx, pb, bound))
 
     def _generate_hess_once(self, tx, pb, bound):
-        if self.n_estimate_terminal != self.n_estimate_integral:
-            raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
+        MT, MI = self.n_estimate_terminal, self.n_estimate_integral
+        if MT != MI:  # the terminal estimators over MT paths + the integral ones over MI (data.py:1164, :845)
+            ws = self.point_baseline(tx, hessians=True)
+            parts = [self.finalize_hessians(*self.label_moments_hessians(tx, pb, M, 0, M, ws, f), M, ws,
+                                            float("inf"), f)
+                     for M, f in ((MT, _lib.DPI_TERMINAL), (MI, _lib.DPI_INTEGRAL))]
+            b = self.sample_bound if bound is None else bound
+            return torch.clamp(parts[0] + parts[1], -b, b)
         n, nx, M = tx.shape[0], self.equation.nx, self.n_estimate_integral
         if M > PATHS_PER_CALL_MAX:  # several calls: baseline, per-range sums, one finalize
             ws = self.point_baseline(tx, hessians=True)

@@ -56,6 +56,29 @@ class ShardedLabeler:
                               "only at power-of-two block counts)", ShardBitIdentityWarning, stacklevel=2)
         return self.rank * per, (self.rank + 1) * per
 
+    def estimator_sets(self, flags=None):
+        """[(M, flags)] of this generator's label passes: one pass over M paths when
+        n_estimate_terminal == n_estimate_integral (or one estimator is asked for), else a
+        DPI_TERMINAL pass over n_estimate_terminal paths and a DPI_INTEGRAL pass over
+        n_estimate_integral paths, whose labels add (picard/data.py:1208-1218; the counts
+        :444, :460, :845, :1164).  Each pass shards its own M across the ranks."""
+        from . import _lib
+        flags = _lib.DPI_BOTH if flags is None else flags
+        MT, MI = self.gen.n_estimate_terminal, self.gen.n_estimate_integral
+        if MT == MI or flags != _lib.DPI_BOTH:
+            return [(MT if flags == _lib.DPI_TERMINAL else MI, flags)]
+        return [(MT, _lib.DPI_TERMINAL), (MI, _lib.DPI_INTEGRAL)]
+
+    def _bound(self):
+        return getattr(self.gen, "sample_bound", float("inf"))
+
+    def _add_clip(self, ys):
+        """Labels of the estimator passes -> their sum, clipped like the reference (data.py:222)."""
+        if len(ys) == 1:
+            return ys[0]
+        b = self._bound()
+        return torch.clamp(ys[0] + ys[1], -b, b)
+
     def gather_moments(self, mom):
         if self.world == 1:
             return mom
@@ -64,6 +87,18 @@ class ShardedLabeler:
         flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
         dist.all_gather_into_tensor(flat, mom, group=self.group)  # rank-major concatenation
         return self.gen.moments_reduce(flat.view((self.world,) + tuple(mom.shape)))
+
+    def _gather_stacked(self, parts, reduce, async_op=False):
+        """One all-gather of this rank's per-pass tensors (same shape), stacked; -> (flat, work)
+        for _reduce_stacked (async) or the per-pass rank-reduced tensors."""
+        import torch.distributed as dist
+        x = torch.stack([p.contiguous() for p in parts]).contiguous()
+        flat = torch.empty((self.world,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        work = dist.all_gather_into_tensor(flat.view((self.world * x.shape[0],) + tuple(x.shape[1:])), x,
+                                           group=self.group, async_op=async_op)
+        if async_op:
+            return flat, work
+        return [reduce(flat[:, k]) for k in range(len(parts))]
 
     def gather_sums(self, x):
         """All-gather per-rank sums (any shape) and reduce them in canonical rank order."""
@@ -98,18 +133,27 @@ class ShardedLabeler:
 
     def _labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
         """generate_with_gradients_and_hessians for tx with this rank's MC shard (n, 1 + nx + nx^2);
-        identical on every rank.  Exchange: the (n, 2, 1+nx) moments and (n, nx^2) Hessian sums."""
-        M = self.gen.n_estimate_integral
-        if self.gen.n_estimate_terminal != M:
-            raise NotImplementedError("Hessian labels need n_estimate_terminal == n_estimate_integral")
+        identical on every rank.  Exchange: the (n, 2, 1+nx) moments and (n, nx^2) Hessian sums (of
+        both estimator passes when n_estimate_terminal != n_estimate_integral)."""
+        sets = self.estimator_sets()
         ws = self.gen.point_baseline(tx, hessians=True)
-        m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
-        mom, hs = self.gen.label_moments_hessians(tx, point_base, M, m0, m1, ws)
+        if len(sets) == 1:
+            M = sets[0][0]
+            mom, hs = self.gen.label_moments_hessians(tx, point_base, M, *self.shard(M), ws)
+            if on_moments_end:
+                on_moments_end()
+            return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
+        sums = [self.gen.label_moments_hessians(tx, point_base, M, *self.shard(M), ws, flags=f) for M, f in sets]
         if on_moments_end:
             on_moments_end()
-        return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
+        if self.world > 1:
+            moms = self._gather_stacked([m for m, _ in sums], self.gen.sums_reduce)
+            hss = self._gather_stacked([h for _, h in sums], self.gen.sums_reduce)
+            sums = list(zip(moms, hss))
+        return self._add_clip([self.gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"), flags=f)
+                               for (mom, hs), (M, f) in zip(sums, sets)])
 
     # ------------------------------------------------------------------ two-phase (pipelined) labels
     def prepare(self, n, flags=None):
@@ -123,8 +167,12 @@ class ShardedLabeler:
         flags = _lib.DPI_BOTH if flags is None else flags
         gen = self.gen
         cur = torch.cuda.current_stream(gen.device)
-        M = gen.n_estimate_integral
-        need = gen.workspace_bytes(n, M)
+        sets = self.estimator_sets(flags)
+        M = max(m for m, _ in sets)
+        # unequal estimator counts run two label passes in begin(): their points and baseline are
+        # prepared here, the passes themselves are not staged
+        staged = len(sets) == 1
+        need = gen.workspace_bytes(n, M, prepared=True)
         if getattr(self, "_prep_ws", None) is None or self._prep_ws[0].numel() < need:
             torch.cuda.synchronize(gen.device)  # a resized pool must not alias in-flight work
             self._side = torch.cuda.Stream(device=gen.device)
@@ -149,15 +197,17 @@ class ShardedLabeler:
                 tx, pb, ev = ahead[3:]
                 self._side.wait_event(ev)
                 tx.record_stream(self._side)
-                gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
-            elif pis or not hasattr(gen, "sample_points_baseline"):  # the staged rollout reads the points
+                if staged:
+                    gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
+            elif pis or not staged or not hasattr(gen, "sample_points_baseline"):  # the staged rollout reads the points
                 if hasattr(gen, "sample_points_baseline"):  # one launch: the sampling inside the baseline's
                     pb = gen._take_points(n)
                     tx = gen.sample_points_baseline(n, pb, ws)
                 else:
                     tx, pb = gen.sample_t_and_x(n)
                     gen.point_baseline(tx, ws=ws)
-                gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
+                if staged:
+                    gen.label_prepare(tx, pb, M, m0, m1, flags, ws)
             else:
                 # fused-kernel nets: the staged part (GBM: the noise sums, dpi_label_prepare) needs no
                 # points, so it is enqueued first and starts beside the previous batch's path launch;
@@ -178,7 +228,7 @@ class ShardedLabeler:
                 ev2 = torch.cuda.Event()
                 ev2.record(self._samp)
             self._ahead = (n, getattr(gen, "seed", None), getattr(gen, "epoch", None), tx2, pb2, ev2)
-        return tx, pb, ws, ready, k, flags
+        return tx, pb, ws, ready, k, flags, staged
 
     def begin(self, tx=None, point_base=None, flags=None, on_moments_begin=None, on_moments_end=None,
               prepared=None):
@@ -187,20 +237,20 @@ class ShardedLabeler:
         kernels while it is in flight).  Two workspaces alternate (three with prepare()), so one
         batch may be pending while the next begins.  Returns the handle end() turns into labels."""
         from . import _lib
-        M = self.gen.n_estimate_integral
-        if self.gen.n_estimate_terminal != M:
-            raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
         slot = wslot = None
         kflags = None
         grp = self._range_group()
         if prepared is not None:
-            tx, point_base, ws, ready, slot, pflags = prepared
+            tx, point_base, ws, ready, slot, pflags, staged = prepared
             if flags is not None and flags != pflags:
                 raise ValueError(f"begin(flags={flags}) on a batch prepared with flags={pflags}")
             flags = pflags
-            kflags = flags | _lib.DPI_PREPARED
+            if staged:
+                kflags = flags | _lib.DPI_PREPARED
             torch.cuda.current_stream(self.gen.device).wait_event(ready)
-        else:
+        sets = self.estimator_sets(flags)
+        M = max(m for m, _ in sets)
+        if prepared is None:
             n = tx.shape[0]
             need = self.gen.workspace_bytes(n, M)
             if not hasattr(self, "_ws_pool") or self._ws_pool[0].numel() < need:
@@ -217,25 +267,27 @@ class ShardedLabeler:
             self._ws_next ^= 1
             self.gen.point_baseline(tx, ws=ws)
         flags = _lib.DPI_BOTH if flags is None else flags
-        m0, m1 = self.shard(M)
         repair = (tx, point_base, flags)  # end() registers labels(tx, point_base, flags) as the repair
         if on_moments_begin:
             on_moments_begin()
         if self.world == 1:  # one rank: the labels come out of the moments' reduce launch
-            y, _ = grp.run(lambda: self.gen.label_moments_finalize(tx, point_base, M,
-                                                                   flags if kflags is None else kflags, ws))
+            if len(sets) == 1:
+                y, _ = grp.run(lambda: self.gen.label_moments_finalize(tx, point_base, M,
+                                                                       flags if kflags is None else kflags, ws))
+            else:
+                y = grp.run(lambda: self._add_clip([self.gen.label_moments_finalize(tx, point_base, m, f, ws,
+                                                                                    bound=float("inf"))[0]
+                                                    for m, f in sets]))
             if on_moments_end:
                 on_moments_end()
-            return (None, y, None, None, flags, M, slot, wslot, grp, repair)  # ws None: y final (end() recycles)
-        mom = grp.run(lambda: self.gen.label_moments(tx, point_base, M, m0, m1, flags if kflags is None else kflags,
-                                                     ws))
+            return (None, y, None, sets, slot, wslot, grp, repair)  # ws None: y final (end() recycles)
+        moms = [grp.run(lambda m=m, f=f: self.gen.label_moments(tx, point_base, m, *self.shard(m),
+                                                                f if kflags is None else kflags, ws))
+                for m, f in sets]
         if on_moments_end:
             on_moments_end()
-        import torch.distributed as dist
-        mom = mom.contiguous()
-        flat = torch.empty((self.world * mom.shape[0],) + tuple(mom.shape[1:]), dtype=mom.dtype, device=mom.device)
-        work = dist.all_gather_into_tensor(flat, mom, group=self.group, async_op=True)
-        return (ws, flat, work, tuple(mom.shape), flags, M, slot, wslot, grp, repair)
+        flat, work = self._gather_stacked(moms, None, async_op=True)
+        return (ws, flat, work, sets, slot, wslot, grp, repair)
 
     def _pipeline_pending(self):
         return any(getattr(self, "_ws_busy", ())) or any(getattr(self, "_prep_busy", ()))
@@ -274,14 +326,14 @@ class ShardedLabeler:
 
     def end(self, pending):
         """Second half: wait for the all-gather, canonical reduce, finalize -> y (n, 1+nx)."""
-        ws, mom, work, shape, flags, M, slot, wslot, grp, (tx, point_base, rflags) = pending
+        ws, flat, work, sets, slot, wslot, grp, (tx, point_base, rflags) = pending
         if ws is None:  # one rank: begin() already finalized
-            y = mom
+            y = flat
         else:
-            if work is not None:
-                work.wait()  # the current stream waits for RCCL's, not the host
-                mom = self.gen.moments_reduce(mom.view((self.world,) + shape))
-            y = self.gen.finalize(mom, M, flags, ws)
+            work.wait()  # the current stream waits for RCCL's, not the host
+            bound = None if len(sets) == 1 else float("inf")
+            y = self._add_clip([self.gen.finalize(self.gen.moments_reduce(flat[:, k]), m, f, ws, bound=bound)
+                                for k, (m, f) in enumerate(sets)])
         if slot is not None:  # prepare() may refill this workspace once the finalize has run
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(self.gen.device))
@@ -298,25 +350,21 @@ class ShardedLabeler:
         return self._guarded(lambda: self._labels(tx, point_base, flags, on_moments_begin, on_moments_end))
 
     def _labels(self, tx, point_base, flags=None, on_moments_begin=None, on_moments_end=None):
-        from . import _lib
-        flags = _lib.DPI_BOTH if flags is None else flags
-        M = self.gen.n_estimate_integral
-        if self.gen.n_estimate_terminal != M:
-            raise NotImplementedError("sharded labels need n_estimate_terminal == n_estimate_integral")
+        sets = self.estimator_sets(flags)
         ws = self.gen.point_baseline(tx)
-        m0, m1 = self.shard(M)
         if on_moments_begin:
             on_moments_begin()
+        bound = None if len(sets) == 1 else float("inf")  # two passes: clip their sum, not each
         if self.world == 1:  # one rank: the labels come out of the moments' reduce launch
-            y, _ = self.gen.label_moments_finalize(tx, point_base, M, flags, ws)
+            ys = [self.gen.label_moments_finalize(tx, point_base, m, f, ws, bound=bound)[0] for m, f in sets]
             if on_moments_end:
                 on_moments_end()
-            return y
-        mom = self.gen.label_moments(tx, point_base, M, m0, m1, flags, ws)
+            return self._add_clip(ys)
+        moms = [self.gen.label_moments(tx, point_base, m, *self.shard(m), f, ws) for m, f in sets]
         if on_moments_end:
             on_moments_end()
-        mom = self.gather_moments(mom)
-        return self.gen.finalize(mom, M, flags, ws)
+        moms = self._gather_stacked(moms, self.gen.moments_reduce)
+        return self._add_clip([self.gen.finalize(mom, m, f, ws, bound=bound) for mom, (m, f) in zip(moms, sets)])
 
     # ------------------------------------------------------------------ batch_data_generator surface
     def sample_labels(self, n_batch, on_moments_begin=None, on_moments_end=None):

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 3
+#define DPI_ABI_VERSION 4
 
 /* error codes */
 #define DPI_OK 0
@@ -182,6 +182,11 @@ int dpi_build_id(char* buf, size_t len);
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
 size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
 
+/* Workspace of dpi_label_prepare and of the DPI_PREPARED dpi_label_moments call it feeds: for a GBM
+ * MLP net it adds the staged noise sums ((n, M / 64, 2, 4 ceil(nx / 4), 64) floats), otherwise it
+ * equals dpi_workspace_bytes. */
+size_t dpi_workspace_bytes_prepared(dpi_problem p, dpi_net net, int n, int M);
+
 /* Draws 1-3 of sample_with_gradients: tx (n, 1+nx) fp32 device, t = (T-2eps)(1-U)+eps,
  * x = x0 + sqrt(t) sqrt(alpha) xi.  Point i uses counter c2 = point_base + i. */
 int dpi_sample_points(dpi_problem p, int n, uint64_t seed, uint32_t epoch, uint32_t point_base, float eps,
@@ -279,11 +284,15 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
  * after dpi_point_baseline, the sums over m in [m_begin, m_end) of the value/gradient
  * contributions and their squares (moments (n, 2, 1+nx)) and of the Hessian contributions
  * (hessian_sums (n, nx*nx)); dpi_label_finalize_hessians turns (possibly rank-reduced) sums into
- * y (n, 1 + nx + nx*nx) = clip(sums / M [+ g(x)]). */
+ * y (n, 1 + nx + nx*nx) = clip(sums / M [+ g(x)]).  flags (ABI 4): DPI_TERMINAL and/or DPI_INTEGRAL
+ * select the estimators (terminal: value/gradient + N1 Hessian term and its identity part, + g(x) at
+ * finalize; integral: the same for f and N2), so n_estimate_terminal != n_estimate_integral runs as
+ * a DPI_TERMINAL pass over M_T paths plus a DPI_INTEGRAL pass over M_I paths, summed
+ * (picard/data.py:1164 vs :845). */
 int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
-                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, float* moments,
+                               uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                                float* hessian_sums, void* ws, size_t ws_bytes, void* stream);
-int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M,
+int dpi_label_finalize_hessians(dpi_problem p, const float* moments, const float* hessian_sums, int n, int M, int flags,
                                 float sample_bound, float* y, void* ws, size_t ws_bytes, void* stream);
 
 /* out[j] = canonical tree sum over the n_parts rows of parts (n_parts, len) (the rank-reduce of

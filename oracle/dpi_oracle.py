@@ -346,12 +346,16 @@ def td_horizon(eq, t, delta_t):
 
 
 def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=1024,
-                return_parts=False, delta_t=0.0):
+                return_parts=False, delta_t=0.0, MT=None):
     """generate_with_gradients (picard/data.py:1208-1218) with K-step EM paths.
 
     Returns y (n, 1+nx) = terminal + integral.  v > 0 enables SDGD indices (GBM).
     delta_t > 0 selects the TD estimators (data.py:1209-1213): horizon t_next = min(t + delta_t, T)
-    instead of T, terminal value u(t_next, X) where t_next < T (data.py:934-952, :529-575)."""
+    instead of T, terminal value u(t_next, X) where t_next < T (data.py:934-952, :529-575).
+    M is n_estimate_integral (data.py:460); MT = n_estimate_terminal (:444, default M): the terminal
+    estimator averages paths m < MT, the integral one m < M."""
+    MT = M if MT is None else MT
+    MI, M = M, max(M, MT)
     tx = np.asarray(tx, np.float64)
     n = tx.shape[0]
     nx = eq.nx
@@ -376,17 +380,23 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
         for m0 in range(0, M, m_chunk):
             m = np.arange(m0, min(M, m0 + m_chunk))
             S_T, S_s, U, idx = path_noise(eq, ig, m, K, seed, epoch, v)
-            # terminal (data.py:899-926; TD :934-952)
-            hT = hmt / K
-            W_T = math.sqrt(hT) * S_T
-            XT = x + a * W_T
-            Y = W_T / hmt / a
-            if td_u:
-                c = net.value_grad(np.concatenate([np.full((len(m), 1), t + delta_t), XT], -1))[0] - g_x
-            else:
-                c = (eq.g(XT) - g_x)
-            term[r, 0] += c.sum()
-            term[r, 1:] += (c * Y).sum(0)
+            kt, ki = m < MT, m < MI
+            S_T, S_s, U = S_T[kt], S_s[ki], U[ki]
+            idx = idx[ki] if idx is not None else None
+            mt, m = m[kt], m[ki]
+            if len(mt):  # terminal (data.py:899-926; TD :934-952)
+                hT = hmt / K
+                W_T = math.sqrt(hT) * S_T
+                XT = x + a * W_T
+                Y = W_T / hmt / a
+                if td_u:
+                    c = net.value_grad(np.concatenate([np.full((len(mt), 1), t + delta_t), XT], -1))[0] - g_x
+                else:
+                    c = (eq.g(XT) - g_x)
+                term[r, 0] += c.sum()
+                term[r, 1:] += (c * Y).sum(0)
+            if not len(m):
+                continue
             # integral (data.py:471-527, 350-366; TD :529-575)
             s = (U * hmt + t)[:, None]
             W_s = np.sqrt((s - t) / K) * S_s
@@ -403,8 +413,8 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
             cI = hmt * (f - fb)
             integ[r, 0] += cI.sum() + (fb * hmt).sum()
             integ[r, 1:] += (cI * Ys).sum(0)
-        term[r] /= M
-        integ[r] /= M
+        term[r] /= MT
+        integ[r] /= MI
         term[r, 0] += g_x
     y = term + integ
     if return_parts:
@@ -415,7 +425,7 @@ def labels_grad(eq, net, tx, M, K, seed, epoch=0, point_base=0, v=0, m_chunk=102
 S_HESS_OFFSET = 1e-4  # picard/data.py:848: s = U (T - t) + t + 0.0001 in the Hessian estimator
 
 
-def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512, return_parts=False):
+def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512, return_parts=False, MT=None):
     """generate_with_gradients_and_hessians (picard/data.py:1220-1223) with K-step EM paths:
     estimate_terminal_with_gradients_and_hessians_double (:1153-1201) +
     estimate_integral_with_gradients_and_hessians_double (:823-897).
@@ -428,7 +438,10 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
         H = mean_m[ dg_m (N1 N1^T - I) + (T - t) df_m (N2 N2^T - I) ]
         dg = (g(x + a sqrt(T-t) N1) + g(x - ...) - 2 g(x)) / 2 / (T - t)
         df = (f(s, x + a sqrt(s-t) N2) + f(s, x - ...) - 2 f(t, x)) / 2 / (s - t)
-    with fresh normals N1 (tag HTERM), N2 (tag HINT).  Returns y (n, 1 + nx + nx^2)."""
+    with fresh normals N1 (tag HTERM), N2 (tag HINT).  Returns y (n, 1 + nx + nx^2).
+    M = n_estimate_integral (:845), MT = n_estimate_terminal (:1164, default M)."""
+    MT = M if MT is None else MT
+    MI, M = M, max(M, MT)
     tx = np.asarray(tx, np.float64)
     n, nx, T, a = tx.shape[0], eq.nx, eq.T, eq.alpha_sqrt
     term = np.zeros((n, 1 + nx))
@@ -444,19 +457,23 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
         f_b = _f_and_extras(eq, net, np.array([[t]]), x)[0][0, 0]
         for m0 in range(0, M, m_chunk):
             m = np.arange(m0, min(M, m0 + m_chunk))
-            B = len(m)
             S_T, S_s, U, _ = path_noise(eq, ig, m, K, seed, epoch)
-            N1 = px.normals(px.TAG_HTERM, epoch, seed, ig, m, 0, nx)
-            N2 = px.normals(px.TAG_HINT, epoch, seed, ig, m, 0, nx)
-            # terminal, value / gradient (:1166-1183)
-            W_T = math.sqrt((T - t) / K) * S_T
-            c = eq.g(x + a * W_T) - g_x
-            term[r, 0] += c.sum()
-            term[r, 1:] += (c * W_T / (T - t)).sum(0)
-            # terminal Hessian (:1185-1199)
-            W1 = math.sqrt(T - t) * N1
-            dg = (eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g_x) / 2 / (T - t)          # (B, 1)
-            hT[r] += np.einsum("b,bi,bj->ij", dg[:, 0], N1, N1) - dg.sum() * eye
+            kt, ki = m < MT, m < MI
+            S_T, S_s, U = S_T[kt], S_s[ki], U[ki]
+            N1 = px.normals(px.TAG_HTERM, epoch, seed, ig, m[kt], 0, nx)
+            N2 = px.normals(px.TAG_HINT, epoch, seed, ig, m[ki], 0, nx)
+            B = int(ki.sum())
+            if kt.any():  # terminal, value / gradient (:1166-1183)
+                W_T = math.sqrt((T - t) / K) * S_T
+                c = eq.g(x + a * W_T) - g_x
+                term[r, 0] += c.sum()
+                term[r, 1:] += (c * W_T / (T - t)).sum(0)
+                # terminal Hessian (:1185-1199)
+                W1 = math.sqrt(T - t) * N1
+                dg = (eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g_x) / 2 / (T - t)          # (B, 1)
+                hT[r] += np.einsum("b,bi,bj->ij", dg[:, 0], N1, N1) - dg.sum() * eye
+            if not B:
+                continue
             # integral, value / gradient (:846-866)
             s = (U * (T - t) + t + S_HESS_OFFSET)[:, None]
             W_s = np.sqrt((s - t) / K) * S_s
@@ -470,10 +487,10 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
             fm = _f_and_extras(eq, net, s, x - a * W2)[0]
             df = (fp + fm - 2 * f_b) / 2 / (s - t)                                       # (B, 1)
             hI[r] += (T - t) * (np.einsum("b,bi,bj->ij", df[:, 0], N2, N2) - df.sum() * eye)
-        term[r] /= M
-        integ[r] /= M
-        hT[r] /= M
-        hI[r] /= M
+        term[r] /= MT
+        integ[r] /= MI
+        hT[r] /= MT
+        hI[r] /= MI
         term[r, 0] += g_x
     y = np.concatenate([term + integ, (hT + hI).reshape(n, nx * nx)], -1)
     if return_parts:
@@ -482,10 +499,10 @@ def labels_grad_hess(eq, net, tx, M, K, seed, epoch=0, point_base=0, m_chunk=512
 
 
 def sample_with_gradients(eq, net, n, M, K, seed, epoch=0, point_base=0, v=0, sample_bound=np.inf, delta_t=0.0,
-                          t_factors=0):
+                          t_factors=0, MT=None):
     """picard/data.py:211-223: (tx, clip(y))."""
     tx = sample_points(eq, n, seed, epoch, point_base, t_factors=t_factors)
-    y = labels_grad(eq, net, tx, M, K, seed, epoch, point_base, v, delta_t=delta_t)
+    y = labels_grad(eq, net, tx, M, K, seed, epoch, point_base, v, delta_t=delta_t, MT=MT)
     return tx, np.clip(y, -sample_bound, sample_bound)
 
 
@@ -500,9 +517,10 @@ def rel_l2_parts(a, b):
 
 
 # ----------------------------------------------------------------------------- moments (sharding)
-def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0, delta_t=0.0):
+def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0, delta_t=0.0, flags=3):
     """Per-path contribution rows c (len(m), 1+nx) whose mean (+ g(x) in column 0) is the label
-    (picard/data.py:923-925, :523-526; TD :947-951, :570-574), for one point and MC indices m."""
+    (picard/data.py:923-925, :523-526; TD :947-951, :570-574), for one point and MC indices m.
+    flags (DPI_TERMINAL = 1 | DPI_INTEGRAL = 2): the estimators included."""
     t = float(tx_row[0])
     x = np.asarray(tx_row[1:], np.float64)[None]
     a = eq.alpha_sqrt
@@ -521,13 +539,18 @@ def path_contributions(eq, net, tx_row, ig, m, K, seed, epoch=0, delta_t=0.0):
     f, _ = _f_and_extras(eq, net, s, x + a * W_s)
     cI = hmt * (f - fb)
     Ys = W_s / (s - t) / a
+    if not flags & 1:
+        cT = 0 * cT
+    if not flags & 2:
+        cI, fb = 0 * cI, 0.0
     c = np.concatenate([cT + cI + fb * hmt, cT * Y + cI * Ys], -1)
     return c, g_x
 
 
-def path_contributions_hess(eq, net, tx_row, ig, m, K, seed, epoch=0):
+def path_contributions_hess(eq, net, tx_row, ig, m, K, seed, epoch=0, flags=3):
     """Per-path rows of the Hessian-label estimator (labels_grad_hess): value/gradient c
-    (len(m), 1+nx), Hessian h (len(m), nx*nx) whose means (+ g(x) in c[:, 0]) are the label."""
+    (len(m), 1+nx), Hessian h (len(m), nx*nx) whose means (+ g(x) in c[:, 0]) are the label.
+    flags (DPI_TERMINAL = 1 | DPI_INTEGRAL = 2): the estimators included."""
     t = float(tx_row[0])
     x = np.asarray(tx_row[1:], np.float64)[None]
     T, a, nx = eq.T, eq.alpha_sqrt, eq.nx
@@ -542,15 +565,17 @@ def path_contributions_hess(eq, net, tx_row, ig, m, K, seed, epoch=0):
     s = (U * (T - t) + t + S_HESS_OFFSET)[:, None]
     W_s = np.sqrt((s - t) / K) * S_s
     cI = (T - t) * (_f_and_extras(eq, net, s, x + a * W_s)[0] - f_b)
-    c = np.concatenate([cT + cI + f_b * (T - t), cT * W_T / (T - t) + cI * W_s / (s - t)], -1)
+    kT, kI = float(flags & 1 != 0), float(flags & 2 != 0)
+    cT, cI = kT * cT, kI * cI
+    c = np.concatenate([cT + cI + kI * f_b * (T - t), cT * W_T / (T - t) + cI * W_s / (s - t)], -1)
     W1 = math.sqrt(T - t) * N1
     aT = ((eq.g(x + a * W1) + eq.g(x - a * W1) - 2 * g_x) / 2 / (T - t))[:, 0]
     W2 = np.sqrt(s - t) * N2
     fp = _f_and_extras(eq, net, s, x + a * W2)[0]
     fm = _f_and_extras(eq, net, s, x - a * W2)[0]
     aI = (T - t) * ((fp + fm - 2 * f_b) / 2 / (s - t))[:, 0]
-    h = (aT[:, None, None] * (N1[:, :, None] * N1[:, None, :] - np.eye(nx))
-         + aI[:, None, None] * (N2[:, :, None] * N2[:, None, :] - np.eye(nx)))
+    h = (kT * aT[:, None, None] * (N1[:, :, None] * N1[:, None, :] - np.eye(nx))
+         + kI * aI[:, None, None] * (N2[:, :, None] * N2[:, None, :] - np.eye(nx)))
     return c, h.reshape(len(m), nx * nx), g_x
 
 

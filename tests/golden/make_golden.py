@@ -86,7 +86,10 @@ class NoiseQueue:
         assert not self.items, f"{len(self.items)} injected draws unused"
 
 
-def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v, t_factors=0):
+def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v, t_factors=0, MT=None):
+    """M = n_estimate_integral, MT = n_estimate_terminal (default M): the terminal draw (#4) has
+    n MT rows, the integral ones n M."""
+    MT = M if MT is None else MT
     i = point_base + np.arange(n)
     if t_factors:  # sample_t (data.py:149-159): torch.rand(n, N - i + 1)
         items = [("rand", px.uniforms_seq(px.TAG_T, epoch, seed, i, 0, t_factors))]
@@ -97,9 +100,9 @@ def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v, t_factors=0):
     items.append(("randn", px.normals(px.TAG_X, epoch, seed, i, 0, 0, nx)))
     ii = i[:, None]
     mm = np.arange(M)[None, :]
-    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, mm, k, nx) for k in range(K))
+    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, np.arange(MT)[None, :], k, nx) for k in range(K))
     S_s = sum(px.normals(px.TAG_INT, epoch, seed, ii, mm, k, nx) for k in range(K))
-    items.append(("randn", (S_T / math.sqrt(K)).reshape(n * M, nx)))
+    items.append(("randn", (S_T / math.sqrt(K)).reshape(n * MT, nx)))
     items.append(("rand", px.uniforms(px.TAG_S, epoch, seed, ii, mm, open_low=True).reshape(n * M, 1)))
     items.append(("randn", (S_s / math.sqrt(K)).reshape(n * M, nx)))
     if v > 0:
@@ -107,21 +110,24 @@ def noise_items(eq_name, nx, n, M, K, seed, epoch, point_base, v, t_factors=0):
     return items
 
 
-def noise_items_hess(nx, n, M, K, seed, epoch, point_base):
+def noise_items_hess(nx, n, M, K, seed, epoch, point_base, MT=None):
     """Draw order of sample_with_gradients_and_hessians (picard/data.py:225-237) for a GBM
     equation: t | x | terminal dW1, dW2 (two half-steps), N1 | s, integral dW1, dW2, N2.  Each
     pair of half-step normals is injected as S / sqrt(2K) twice, so the two half-steps sum to the
-    K-step endpoint x + a sqrt((tau - t)/K) S."""
+    K-step endpoint x + a sqrt((tau - t)/K) S.  Terminal draws n MT rows (n_estimate_terminal,
+    :1164), integral ones n M (:845)."""
+    MT = M if MT is None else MT
     i = point_base + np.arange(n)
     items = [("rand", px.uniforms(px.TAG_T, epoch, seed, i, 0)[:, None]),
              ("randn", px.normals(px.TAG_X, epoch, seed, i, 0, 0, nx))]
     ii = i[:, None]
     mm = np.arange(M)[None, :]
-    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, mm, k, nx) for k in range(K)).reshape(n * M, nx)
+    mt = np.arange(MT)[None, :]
+    S_T = sum(px.normals(px.TAG_TERM, epoch, seed, ii, mt, k, nx) for k in range(K)).reshape(n * MT, nx)
     S_s = sum(px.normals(px.TAG_INT, epoch, seed, ii, mm, k, nx) for k in range(K)).reshape(n * M, nx)
     half = 1.0 / math.sqrt(2 * K)
     items += [("randn", S_T * half), ("randn", S_T * half),
-              ("randn", px.normals(px.TAG_HTERM, epoch, seed, ii, mm, 0, nx).reshape(n * M, nx)),
+              ("randn", px.normals(px.TAG_HTERM, epoch, seed, ii, mt, 0, nx).reshape(n * MT, nx)),
               ("rand", px.uniforms(px.TAG_S, epoch, seed, ii, mm, open_low=True).reshape(n * M, 1)),
               ("randn", S_s * half), ("randn", S_s * half),
               ("randn", px.normals(px.TAG_HINT, epoch, seed, ii, mm, 0, nx).reshape(n * M, nx))]
@@ -155,7 +161,7 @@ def state_dict_np(module):
 
 def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, point_base=0, v=0,
              init_seed=0, workdir=None, zero=False, weight_scale=1.0, hessians=False, delta_t=0.0, picard_N=1,
-             picard_i=1, t_uniform=True):
+             picard_i=1, t_uniform=True, homog=None, MT=None):
     torch.set_default_dtype(torch.float64)
     eq = make_equation(eq_name, eq_kw, workdir)
     torch.manual_seed(init_seed)
@@ -170,25 +176,36 @@ def run_case(name, eq_name, eq_kw, net_kind, net_kw, n, M, K, seed, epoch=0, poi
         with torch.no_grad():
             for p in net.parameters():
                 p.mul_(weight_scale)
+    if homog is not None:  # the network's first layer x s, its other hidden biases x s, its output weights x 1/s:
+        # about the same function with every hidden activation ~s times smaller (tools/probe_small.py)
+        seq = net.nn_module if net_kind == "pis" else net
+        lin = [m for m in seq if isinstance(m, torch.nn.Linear)]
+        with torch.no_grad():
+            lin[0].weight.mul_(homog)
+            for m in lin[:-1]:
+                m.bias.mul_(homog)
+            lin[-1].weight.mul_(1.0 / homog)
     if net_kind == "pis" and not zero:
         with torch.no_grad():  # a non-trivial learnable phase
             net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
     hess = CfgNode({"method": "SDGD" if v > 0 else None, "kwargs": CfgNode({"v": v} if v > 0 else {})})
     gen = data.OnlineDataGenerator(
-        eq, net, picard_N, picard_i, device="cpu", t_always_uniform=t_uniform, n_estimate_terminal=M,
+        eq, net, picard_N, picard_i, device="cpu", t_always_uniform=t_uniform,
+        n_estimate_terminal=M if MT is None else MT,
         n_estimate_integral=M, hessian_approximation=hess, sample_bound=None,
         estimate_terminal="OU_ByGx", estimate_integral="OU_Simple", estimate_delta_t=delta_t)
     if hessians:
-        items = noise_items_hess(eq.nx, n, M, K, seed, epoch, point_base)
+        items = noise_items_hess(eq.nx, n, M, K, seed, epoch, point_base, MT)
         with NoiseQueue(items):
             tx, y = gen.sample_with_gradients_and_hessians(n)
     else:
         t_factors = 0 if t_uniform else picard_N - picard_i + 1
-        items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v, t_factors)
+        items = noise_items(eq_name, eq.nx, n, M, K, seed, epoch, point_base, v, t_factors, MT)
         with NoiseQueue(items):
             tx, y = gen.sample_with_gradients(n)
     out = {
         "case": name, "eq": eq_name, "net": "zero" if zero else net_kind, "n": n, "M": M, "K": K,
+        "MT": M if MT is None else MT,
         "seed": np.uint64(seed), "epoch": epoch, "point_base": point_base, "v": v, "hessians": hessians,
         "delta_t": delta_t, "t_factors": 0 if (t_uniform or hessians) else picard_N - picard_i + 1,
         "tx": tx.numpy(), "y": y.detach().numpy(),
@@ -245,6 +262,35 @@ def main(only=None):
              weight_scale=8.0)
     run_case("ou_pis32_ws32_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 64, 2, 44, workdir=wd,
              weight_scale=32.0)
+    # small magnitudes in the split storage: every parameter x 1/16 and x 1/256
+    # ("wsd"), and the network rescaled so every hidden activation is ~1/256 as large ("homog")
+    for s, tag in ((1 / 16, "wsd16"), (1 / 256, "wsd256")):
+        run_case(f"ou_pis32_{tag}_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 64, 2, 61, workdir=wd,
+                 weight_scale=s)
+        run_case(f"gbm_mlp16_sdgd_{tag}_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 2, 64, 2,
+                 62, v=100, workdir=wd, weight_scale=s)
+        run_case(f"gbm_mlp64x3_sdgd_{tag}_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [64] * 3}, 2, 64, 2,
+                 63, v=100, workdir=wd, weight_scale=s)
+        run_case(f"gbm_hess_mlp32x3_{tag}_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [32] * 3}, 2, 64, 2,
+                 64, workdir=wd, weight_scale=s, hessians=True)
+    run_case("ou_pis32_homog256_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 64, 2, 65, workdir=wd,
+             homog=1 / 256)
+    run_case("gbm_mlp64x3_sdgd_homog256_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [64] * 3}, 2, 64, 2,
+             66, v=100, workdir=wd, homog=1 / 256)
+    run_case("gbm_hess_mlp32x3_homog256_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [32] * 3}, 2, 64, 2,
+             67, workdir=wd, homog=1 / 256, hessians=True)
+    run_case("cha_mlp128x4_homog256_K3", "Cha", cha, "mlp", {"neurons": [128] * 4}, 2, 64, 3, 68, workdir=wd,
+             homog=1 / 256)
+    # n_estimate_terminal != n_estimate_integral (data.py:444 / :460, :1164 / :845): terminal over MT paths
+    run_case("cha_mlp16_MT2x_K2", "Cha", cha, "mlp", {"neurons": [16, 16]}, 3, 64, 2, 71, workdir=wd, MT=128)
+    run_case("ou_pis32_MTh_K2", "OUProcessEquation", ou, "pis", {"neurons": [32, 32]}, 2, 128, 2, 72, workdir=wd,
+             MT=64)
+    run_case("gbm_mlp64x3_sdgd_MT2x_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [64] * 3}, 2, 64, 2, 73,
+             v=100, workdir=wd, MT=128)
+    run_case("gbm_hess_mlp32x3_MT2x_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [32] * 3}, 2, 64, 2, 74,
+             workdir=wd, hessians=True, MT=128)
+    run_case("gbm_hess_mlp16_MTh_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16]}, 2, 128, 2, 75,
+             workdir=wd, hessians=True, MT=64)
     # Fully-nonlinear case_1 (GBM): SDGD v=100 and full-Hessian (v=0), MLP 3x16
     run_case("gbm_mlp16_sdgd_K2", "GBMEquationComplexExact", gbm, "mlp", {"neurons": [16, 16, 16]}, 3, 64, 2, 3,
              v=100, workdir=wd)

@@ -28,6 +28,11 @@ def t_factors(f):
     return int(f["t_factors"]) if "t_factors" in f else 0
 
 
+def m_terminal(f):
+    """n_estimate_terminal of a fixture (M, its n_estimate_integral, unless the fixture names it)."""
+    return int(f["MT"]) if "MT" in f else int(f["M"])
+
+
 def delta_t(f):
     """DATA.ESTIMATE_DELTA_T of a fixture (0 = the plain estimators; TD fixtures td_*)."""
     return float(f["delta_t"]) if "delta_t" in f else 0.0

@@ -3,7 +3,7 @@ import numpy as np
 import torch
 
 import deeppicarditeration_amd as dpi
-from golden_util import acts, delta_t, state_dict, t_factors
+from golden_util import acts, delta_t, m_terminal, state_dict, t_factors
 
 
 def product_equation(f):
@@ -37,12 +37,15 @@ def product_module(f, eq):
 
 
 def generator(f, eq, module, M=None, K=None):
+    """The fixture's generator; M overrides both estimator counts (else the fixture's
+    n_estimate_integral M and n_estimate_terminal MT)."""
+    MT = m_terminal(f) if M is None else M
     M = int(f["M"]) if M is None else M
     v = int(f["v"])
     hess = {"method": "SDGD", "kwargs": {"v": v}} if v > 0 else None
     R = t_factors(f)  # sample_t fixtures: a Picard (N, i) with N - i + 1 = R
     return dpi.OnlineDataGenerator(eq, module, R if R else 1, 1, device="cuda:0", t_always_uniform=R == 0,
-                                   n_estimate_terminal=M,
+                                   n_estimate_terminal=MT,
                                    n_estimate_integral=M, n_euler_steps=int(f["K"]) if K is None else K,
                                    seed=int(f["seed"]), epoch=int(f["epoch"]), hessian_approximation=hess,
                                    estimate_delta_t=delta_t(f))

@@ -101,6 +101,16 @@ def test_library_is_built_from_this_tree():
     lib = _lib.load()
     assert _lib.build_id(lib) == B.source_hash()
     assert not B.needs_build()
+    assert B.embedded_id() == B.source_hash()
+
+
+def test_stale_library_needs_build_whatever_the_side_file_says(monkeypatch):
+    """a checkout that changes csrc leaves the old .so in place; needs_build() reads
+    the id embedded in the .so, so a stale library is rebuilt even if a .buildid file says
+    otherwise."""
+    from deeppicarditeration_amd import build as B
+    monkeypatch.setattr(B, "source_hash", lambda: "0" * 64)
+    assert B.needs_build()
 
 
 def test_load_refuses_a_library_built_from_other_sources(monkeypatch):

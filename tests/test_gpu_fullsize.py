@@ -179,3 +179,66 @@ def test_hjb_fused_chain_equals_layer_wise_chain(n, M, monkeypatch):
     assert torch.isfinite(out["1"][1]).all()
     assert torch.equal(out["0"][0], out["1"][0])
     assert torch.equal(out["0"][1], out["1"][1])
+
+
+def test_gbm_hessian_labels_unequal_counts_full_size():
+    """n_estimate_terminal = 2,048 != n_estimate_integral = 1,024 (picard/data.py:1164 vs :845) at
+    configs[4]'s 64 points, K = 50, 3 x 64 ELU: a DPI_TERMINAL pass over 2,048 paths plus a
+    DPI_INTEGRAL pass over 1,024 (dpi_label_moments_hessians flags); the first and last point's value,
+    gradient and Hessian blocks within rel-L2 1e-4 of the fp64 oracle with separate counts, and
+    the sharded labeler's 2 / 4 MC shards of each pass reduce to the same labels bit for bit."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd import _lib as L
+    from oracle import dpi_oracle as O
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    torch.manual_seed(3)
+    net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+    n, MT, MI, K = 64, 2048, 1024, 50
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=MT,
+                                  n_estimate_integral=MI, n_euler_steps=K, seed=1)
+    tx, _ = gen.sample_t_and_x(n, point_base=0)
+    y = gen.generate_with_gradients_and_hessians(tx, point_base=0)
+    assert torch.equal(y, gen.generate_with_gradients_and_hessians(tx, point_base=0))
+    ws = gen.point_baseline(tx, hessians=True)
+    for G in (2, 4):  # each pass's MC range in G shards, reduced per pass, as ShardedLabeler does
+        ys = []
+        for M, f in ((MT, L.DPI_TERMINAL), (MI, L.DPI_INTEGRAL)):
+            parts = [gen.label_moments_hessians(tx, 0, M, r * M // G, (r + 1) * M // G, ws, f) for r in range(G)]
+            mom = gen.sums_reduce(torch.stack([p[0] for p in parts]))
+            hs = gen.sums_reduce(torch.stack([p[1] for p in parts]))
+            ys.append(gen.finalize_hessians(mom, hs, M, ws, float("inf"), f))
+        assert torch.equal(ys[0] + ys[1], y), G
+    y = y.cpu().double().numpy()
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
+                 ["ELU"] * 3)
+    oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+    txh = tx.cpu().double().numpy()
+    for i in (0, n - 1):
+        ref = O.labels_grad_hess(oeq, onet, txh[i:i + 1], MI, K, 1, 1, i, m_chunk=256, MT=MT)
+        ev, eg, eh = (_rel(y[i:i + 1, :1], ref[:, :1]), _rel(y[i:i + 1, 1:101], ref[:, 1:101]),
+                      _rel(y[i:i + 1, 101:], ref[:, 101:]))
+        print(f"point {i}: value {ev:.2e} grad {eg:.2e} hessian {eh:.2e}")
+        assert ev < TOL and eg < TOL and eh < TOL, (i, ev, eg, eh)
+
+
+def test_sharded_labeler_unequal_counts_equal_generator():
+    """ShardedLabeler (one rank) with n_estimate_terminal = 2 n_estimate_integral: labels(), the
+    prepare/begin/end pipeline and labels_hessians equal the generator's own labels bit for bit."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+    torch.manual_seed(5)
+    net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=512,
+                                  n_estimate_integral=256, n_euler_steps=4, seed=2,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": 100}})
+    lab = ShardedLabeler(gen)
+    tx, pb = gen.sample_t_and_x(5)
+    y = gen.generate_with_gradients(tx, point_base=pb)
+    assert torch.equal(lab.labels(tx, pb), y)
+    prep = lab.prepare(5)
+    txp, pbp = prep[0], prep[1]
+    yp = lab.end(lab.begin(prepared=prep))
+    assert torch.equal(yp, gen.generate_with_gradients(txp, point_base=pbp))
+    assert torch.equal(lab.labels_hessians(tx, pb), gen.generate_with_gradients_and_hessians(tx, point_base=pb))

@@ -263,3 +263,140 @@ def test_range_group_fp32_overflow_raises():
         warnings.simplefilter("ignore")
         with pytest.raises(DPIError, match="fp32"):
             grp.verify()
+
+
+# ------------------------------------------------- small magnitudes
+# Networks scaled DOWN: every parameter x 1/16 and x 1/256 ("wsd"), and rescaled so every hidden
+# activation is ~1/256 as large while the function stays about the same ("homog": first layer x s,
+# the other hidden biases x s, output weights x 1/s).  The split storage keeps each operand at a
+# calibrated power-of-two scale (dpi_kernels.hip x3_exponent), so its labels must stay fp32-class:
+# within 10x of the exact-fp32 mode's rel-L2 on the same inputs (or 2e-7, the labels' own fp32
+# rounding, whichever is larger), and within the 1e-4 bar.
+SMALL = ["ou_pis32_wsd16_K2", "ou_pis32_wsd256_K2", "ou_pis32_homog256_K2", "gbm_mlp16_sdgd_wsd16_K2",
+         "gbm_mlp16_sdgd_wsd256_K2", "gbm_mlp64x3_sdgd_wsd16_K2", "gbm_mlp64x3_sdgd_wsd256_K2",
+         "gbm_mlp64x3_sdgd_homog256_K2", "cha_mlp128x4_homog256_K3"]
+SMALL_HESS = ["gbm_hess_mlp32x3_wsd16_K2", "gbm_hess_mlp32x3_wsd256_K2", "gbm_hess_mlp32x3_homog256_K2"]
+FP32_CLASS = 10.0
+FLOOR = 2e-7
+
+
+def _both_modes(label):
+    """label() -> labels, evaluated in split (auto) then exact-fp32 mode."""
+    from deeppicarditeration_amd import _lib as L
+    lib = L.load()
+    out = {}
+    try:
+        for name, mode in (("auto", L.DPI_GEMM_AUTO), ("f32", L.DPI_GEMM_F32)):
+            L.check(lib.dpi_set_gemm_precision(mode), "prec")
+            with warnings.catch_warnings():
+                warnings.simplefilter("error")  # no range fallback: the split itself must hold
+                out[name] = label()
+    finally:
+        L.check(lib.dpi_set_gemm_precision(L.DPI_GEMM_AUTO), "prec")
+    return out
+
+
+def _assert_fp32_class(errs, blocks):
+    for b in blocks:
+        a, f = errs["auto"][b], errs["f32"][b]
+        assert a < TOL and a <= max(FP32_CLASS * f, FLOOR), (b, errs)
+
+
+@pytest.mark.parametrize("case", SMALL + SMALL_HESS)
+def test_down_scaled_goldens_split_is_fp32_class(case):
+    from golden_util import load
+    from gpu_util import generator, product_equation, product_module
+    f = load(case)
+    eq = product_equation(f)
+    tx = torch.as_tensor(f["tx"], dtype=torch.float32, device="cuda:0")
+    hess = case in SMALL_HESS
+
+    def label():
+        gen = generator(f, eq, product_module(f, eq))
+        if hess:
+            return gen.generate_with_gradients_and_hessians(tx, point_base=int(f["point_base"])).cpu().numpy()
+        return gen.generate_with_gradients(tx, point_base=int(f["point_base"])).cpu().numpy()
+
+    ys = _both_modes(label)
+    blocks = {"value": slice(0, 1), "grad": slice(1, 101), "hess": slice(101, None)}
+    errs = {m: {b: _rel(y[:, sl], f["y"][:, sl]) for b, sl in blocks.items() if hess or b != "hess"}
+            for m, y in ys.items()}
+    print(case, errs)
+    _assert_fp32_class(errs, errs["auto"].keys())
+
+
+def _scale_down(lin, s, how):
+    with torch.no_grad():
+        if how == "all":
+            for m in lin:
+                m.weight.mul_(s)
+                m.bias.mul_(s)
+        else:  # homog
+            lin[0].weight.mul_(s)
+            for m in lin[:-1]:
+                m.bias.mul_(s)
+            lin[-1].weight.mul_(1.0 / s)
+
+
+@pytest.mark.parametrize("s, how", [(1 / 16, "all"), (1 / 256, "all"), (1 / 256, "homog"), (1 / 4096, "homog")])
+def test_down_scaled_pisgradnet_4x512_vs_oracle(s, how):
+    """PISGradNet 4 x 512 (configs[2]'s network, the fused k_pis_net chain) scaled down, both modes,
+    against the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.OUProcessEquation(nx=100, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                               alpha_scale=4.0)
+    torch.manual_seed(7)
+    net = dpi.PISGradNet(hidden_shapes=[512] * 4, dim=100, g0=eq.g, T=1.0)
+    with torch.no_grad():
+        net.timestep_phase.copy_(0.1 * torch.randn(1, 64))
+    _scale_down([m for m in net.nn_module if isinstance(m, torch.nn.Linear)], s, how)
+    oeq = O.OUProcessEquation(100, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+    onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
+    tx = None
+
+    def label():
+        nonlocal tx
+        gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                      n_estimate_integral=128, n_euler_steps=10, seed=2)
+        tx, y = gen.sample_with_gradients(2)
+        return y.cpu().double().numpy()
+
+    ys = _both_modes(label)
+    ref = O.labels_grad(oeq, onet, tx.cpu().double().numpy(), 128, 10, 2, 1, 0)
+    errs = {m: {"value": _rel(y[:, :1], ref[:, :1]), "grad": _rel(y[:, 1:], ref[:, 1:])} for m, y in ys.items()}
+    print(f"pis x{s} {how}", errs)
+    _assert_fp32_class(errs, ("value", "grad"))
+
+
+@pytest.mark.parametrize("s, how", [(1 / 16, "all"), (1 / 256, "all"), (1 / 256, "homog"), (1 / 4096, "homog")])
+@pytest.mark.parametrize("hess", [False, True])
+def test_down_scaled_gbm_3x64_vs_oracle(s, how, hess):
+    """GBM 3 x 64 (configs[4]'s network: the split SDGD tangent sweep, and the Malliavin Hessian
+    labels' three sweeps) scaled down, both modes, against the fp64 oracle."""
+    import deeppicarditeration_amd as dpi
+    eq = dpi.GBMEquationComplexExact(100)
+    oeq = O.GBMEquationComplexExact(100, eq.w.numpy(), eq.v.numpy())
+    torch.manual_seed(3)
+    net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+    lin = [m for m in net if isinstance(m, torch.nn.Linear)]
+    _scale_down(lin, s, how)
+    onet = O.MLP([m.weight.detach().double().numpy() for m in lin], [m.bias.detach().double().numpy() for m in lin],
+                 ["ELU"] * 3)
+    tx = None
+
+    def label():
+        nonlocal tx
+        gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                      n_estimate_integral=256, n_euler_steps=10, seed=1,
+                                      hessian_approximation=None if hess else {"method": "SDGD", "kwargs": {"v": 100}})
+        tx, y = gen.sample_with_gradients_and_hessians(2) if hess else gen.sample_with_gradients(2)
+        return y.cpu().double().numpy()
+
+    ys = _both_modes(label)
+    txh = tx.cpu().double().numpy()
+    ref = O.labels_grad_hess(oeq, onet, txh, 256, 10, 1, 1, 0) if hess else O.labels_grad(oeq, onet, txh, 256, 10, 1,
+                                                                                         1, 0, v=100)
+    blocks = {"value": slice(0, 1), "grad": slice(1, 101), "hess": slice(101, None)}
+    errs = {m: {b: _rel(y[:, sl], ref[:, sl]) for b, sl in blocks.items() if hess or b != "hess"} for m, y in ys.items()}
+    print(f"gbm x{s} {how} hess={hess}", errs)
+    _assert_fp32_class(errs, errs["auto"].keys())

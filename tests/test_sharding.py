@@ -44,7 +44,8 @@ class OracleGen:
         out = np.zeros((tx.shape[0], 2, NX + 1), np.float32)
         gx = []
         for r in range(tx.shape[0]):
-            c, g = O.path_contributions(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), K, 7)
+            c, g = O.path_contributions(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), K, 7,
+                                        flags=flags & 3)
             gx.append(g)
             blocks = c.reshape(-1, 64, NX + 1)
             s1 = np.stack([O.tree_sum_f32(bk.astype(np.float32)) for bk in blocks])  # per-block sums
@@ -57,12 +58,13 @@ class OracleGen:
     def moments_reduce(self, parts):
         return torch.from_numpy(O.tree_sum_f32(parts.numpy()))
 
-    def finalize(self, mom, M_, flags, ws):
+    def finalize(self, mom, M_, flags, ws, bound=None):
         y = mom[:, 0].numpy() / M_
-        y[:, 0] += self.gx
+        if flags & 1:  # the terminal estimator adds g(x) (data.py:925)
+            y[:, 0] += self.gx
         return torch.from_numpy(y)
 
-    def label_moments_finalize(self, tx, point_base, M_, flags, ws):
+    def label_moments_finalize(self, tx, point_base, M_, flags, ws, bound=None):
         """The single-rank call (dpi_label_moments_finalize): all of [0, M), finalized."""
         mom = self.label_moments(tx, point_base, M_, 0, M_, flags, ws)
         return self.finalize(mom, M_, flags, ws), mom
@@ -72,9 +74,10 @@ class OracleGenTwoPhase(OracleGen):
     """For begin()/end(): g(x) per batch is recomputed at finalize (the device path keeps it in the
     batch's own workspace)."""
 
-    def finalize(self, mom, M_, flags, ws):
+    def finalize(self, mom, M_, flags, ws, bound=None):
         y = mom[:, 0].numpy() / M_
-        y[:, 0] += self.eq.g(self._tx[:, 1:])[:, 0]
+        if flags & 1:
+            y[:, 0] += self.eq.g(self._tx[:, 1:])[:, 0]
         return torch.from_numpy(y)
 
     def label_moments(self, tx, point_base, M_, m0, m1, flags, ws):
@@ -200,13 +203,14 @@ class OracleGenHess:
         assert hessians
         return tx
 
-    def label_moments_hessians(self, tx, point_base, M_, m0, m1, ws):
+    def label_moments_hessians(self, tx, point_base, M_, m0, m1, ws, flags=3):
         n = tx.shape[0]
         mom = np.zeros((n, 2, NX + 1), np.float32)
         hs = np.zeros((n, NX * NX), np.float32)
         gx = []
         for r in range(n):
-            c, h, g = O.path_contributions_hess(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), KH, 9)
+            c, h, g = O.path_contributions_hess(self.eq, self.net, tx[r], point_base + r, np.arange(m0, m1), KH, 9,
+                                                flags=flags)
             gx.append(g)
             cb, hb = c.reshape(-1, 64, NX + 1), h.reshape(-1, 64, NX * NX)
             mom[r, 0] = O.tree_sum_f32(np.stack([O.tree_sum_f32(b.astype(np.float32)) for b in cb]))
@@ -218,9 +222,10 @@ class OracleGenHess:
     def sums_reduce(self, parts):
         return torch.from_numpy(O.tree_sum_f32(parts.numpy()))
 
-    def finalize_hessians(self, mom, hs, M_, ws):
+    def finalize_hessians(self, mom, hs, M_, ws, bound=None, flags=3):
         y = mom[:, 0].numpy() / M_
-        y[:, 0] += self.gx
+        if flags & 1:
+            y[:, 0] += self.gx
         return torch.from_numpy(np.concatenate([y, hs.numpy() / M_], -1))
 
 
@@ -319,3 +324,71 @@ def test_power_of_two_shards_do_not_warn():
         for G in (1, 2, 4, 8):
             for r in range(G):
                 ShardedLabeler(None, r, G).shard(4096)
+
+
+# ------------------------------------------- n_estimate_terminal != n_estimate_integral
+MT2, MI2 = 256, 128  # the terminal estimator over twice the integral's paths
+
+
+def _worker_unequal(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    g = OracleGenTwoPhase(eq, net)
+    g.n_estimate_terminal, g.n_estimate_integral = MT2, MI2
+    lab = ShardedLabeler(g, rank=rank, world=world)
+    y = lab.labels(tx, 0).numpy()
+    pa = lab.begin(tx, 0)
+    pb = lab.begin(tx, 100)
+    ya, yb = lab.end(pa).numpy(), lab.end(pb).numpy()
+    eqh, neth, txh = _problem_hess()
+    gh = OracleGenHess(eqh, neth)
+    gh.n_estimate_terminal, gh.n_estimate_integral = 2 * MH, MH
+    yh = ShardedLabeler(gh, rank=rank, world=world).labels_hessians(txh, 0).numpy()
+    q.put((rank, y, ya, yb, yh))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_unequal_estimator_counts():
+    """n_estimate_terminal = 2 n_estimate_integral: each estimator pass shards its own M over the
+    ranks (one all-gather of both passes' moments); labels(), the begin()/end() pipeline and the
+    Hessian labels equal the single-rank labels bit for bit on every rank, and the oracle's labels
+    with separate counts (labels_grad / labels_grad_hess MT=) to fp32 summation error."""
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, tx = _problem()
+    g1 = OracleGenTwoPhase(eq, net)
+    g1.n_estimate_terminal, g1.n_estimate_integral = MT2, MI2
+    single = ShardedLabeler(g1, 0, 1).labels(tx, 0).numpy()
+    single_b = ShardedLabeler(g1, 0, 1).labels(tx, 100).numpy()
+    eqh, neth, txh = _problem_hess()
+    gh = OracleGenHess(eqh, neth)
+    gh.n_estimate_terminal, gh.n_estimate_integral = 2 * MH, MH
+    single_h = ShardedLabeler(gh, 0, 1).labels_hessians(txh, 0).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 31000 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker_unequal, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        y, ya, yb, yh = res[r]
+        assert y.tobytes() == single.tobytes() and ya.tobytes() == single.tobytes(), r
+        assert yb.tobytes() == single_b.tobytes(), r
+        assert yh.tobytes() == single_h.tobytes(), r
+    assert O.rel_l2(single, O.labels_grad(eq, net, tx, MI2, K, 7, MT=MT2)) < 1e-5
+    assert O.rel_l2(single_h, O.labels_grad_hess(eqh, neth, txh, MH, KH, 9, MT=2 * MH)) < 1e-5
+
+
+def test_estimator_sets():
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    eq, net, _ = _problem()
+    g = OracleGen(eq, net)
+    assert ShardedLabeler(g).estimator_sets() == [(M, 3)]
+    g.n_estimate_terminal = 2 * M
+    assert ShardedLabeler(g).estimator_sets() == [(2 * M, 1), (M, 2)]
+    assert ShardedLabeler(g).estimator_sets(1) == [(2 * M, 1)]
+    assert ShardedLabeler(g).estimator_sets(2) == [(M, 2)]
