@@ -651,23 +651,6 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   }
 }
 
-// Phase stamps of the GBM network launch (measurement variant only, tools/gbm_stamps.py): lanes 0-1
-// of each wave write s_memtime at fixed points into a device array (vector stores; lane-indexed).
-#ifdef DPI_GBM_STAMPS
-constexpr int DPI_STAMP_BLOCKS = 1024, DPI_STAMP_EV = 8;
-__device__ unsigned long long dpi_stamps[DPI_STAMP_BLOCKS * 4 * DPI_STAMP_EV * 2];
-#define DPI_STAMP(on, ev)                                                                                   \
-  do {                                                                                                      \
-    if ((on) && (threadIdx.x & 63) < 2 && blockIdx.x < DPI_STAMP_BLOCKS)                                    \
-      dpi_stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * DPI_STAMP_EV + (ev)) * 2 + (threadIdx.x & 1)] =    \
-          __builtin_amdgcn_s_memtime();                                                                     \
-  } while (0)
-#else
-#define DPI_STAMP(on, ev) \
-  do {                    \
-  } while (0)
-#endif
-
 // LDS of the fully-nonlinear (GBM) path kernel: every weight matrix stays resident for the
 // 100-direction tangent sweep.  H <= 64, L <= 4.
 template <int H>
@@ -845,10 +828,6 @@ template <int H, int L, int ACT>
 __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
                                                 float& s1_out, float& s2_out) {
   static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
-#ifdef DPI_ABL_NOHDIAG  // measurement variant (tools/build_variant.py): no Hessian diagonal at all
-  s1_out = s2_out = 0.f;
-  return;
-#endif
   constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
   constexpr int WXS = LdsGbm<H>::WXS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1023,37 +1002,9 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
     for (int l = 1; l < L; ++l) {
       half8 bh[NU], bl[NU];
-#ifdef DPI_GBM_TANGENT_2TERM
-      // measurement variant: the tangent operand as fp16 hi only, two products
-      // W_hi z_hi + W_lo z_hi per chunk; gated by the oracle (tools/build_variant.py)
-      {
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-          float v[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = fz[l - 1][2 * u][r] * z[2 * u][r];
-            v[4 + r] = fz[l - 1][2 * u + 1][r] * z[2 * u + 1][r];
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) bh[u][j] = (_Float16)v[j];
-        }
-      }
-      floatx4 o[HT];
-#pragma unroll
-      for (int T = 0; T < HT; ++T) o[T] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-#pragma unroll
-        for (int T = 0; T < HT; ++T) o[T] = mfma16(wh[l - 1][T][u], bh[u], o[T]);
-#pragma unroll
-        for (int T = 0; T < HT; ++T) o[T] = mfma16(wl[l - 1][T][u], bh[u], o[T]);
-      }
-#else
       split_b(z, fz[l - 1], bh, bl);
       floatx4 o[HT];
       wmul(l, bh, bl, o);
-#endif
 #pragma unroll
       for (int T = 0; T < HT; ++T)
 #pragma unroll
@@ -1076,15 +1027,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
   // directions take the full sweep.
   int ndp = e.nx, kmax = e.nx;
   bool lists = false;
-#ifdef DPI_ABL_NOSWEEP  // measurement variant (tools/build_variant.py): no direction sweep
-  s1_out = s2_out = 0.f;
-  return;
-#endif
-#ifdef DPI_ABL_NOLISTS  // measurement variant: the full 100-direction sweep
-  if (false) {
-#else
   if (e.sdgd_v > 0) {
-#endif
     constexpr int DLCAP = LdsGbm<H>::DLCAP;
     // the path's four lanes build its list together: lane qq scans dims [qq dq, (qq + 1) dq) (all
     // its histogram bytes read at once), places its sampled dims after the lower quarters' counts
@@ -1117,7 +1060,6 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     for (int o = 1; o < 64; o <<= 1) kmax = max(kmax, __shfl_xor(kmax, o, 64));
     lists = kmax <= DLCAP;
   }
-  DPI_STAMP(true, 3);
   if (lists) {
     constexpr int DLCAP = LdsGbm<H>::DLCAP;
     auto dir = [&](int k) { return (int)sh.dl[pp * DLCAP + min(k, ndp - 1)]; };
@@ -1139,7 +1081,6 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     }
     if (d < e.nx) direction(d, za, zb, d, true);
   }
-  DPI_STAMP(true, 4);
   s1_out = s1;
   s2_out = s2;
 }
@@ -1281,20 +1222,6 @@ __device__ __forceinline__ float block_sum_b(float v, float* red) {
   return a;
 }
 
-// Phase stamps of k_baseline (measurement variant only, tools/base_stamps.py): thread 0 of each of
-// the first 512 blocks writes s_memtime at fixed points (after the barrier that closes a phase).
-#ifdef DPI_BASE_STAMPS
-__device__ unsigned long long dpi_bstamps[512 * 16];
-#define DPI_BSTAMP(ev)                                                                              \
-  do {                                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x < 512) dpi_bstamps[blockIdx.x * 16 + (ev)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define DPI_BSTAMP(ev) \
-  do {                 \
-  } while (0)
-#endif
-
 // Baseline per point (one workgroup per point): g(x), the state-dependent part of
 // f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
 // f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
@@ -1314,7 +1241,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
   __shared__ float ts;
   const int i = blockIdx.x, tid = threadIdx.x;
   const int nx = e.nx, F = 1 + nx;
-  DPI_BSTAMP(0);
   if (tickets && tid == 0) tickets[i] = 0;
   if (smp.tx) {
     const uint32_t ig = smp.point_base + (uint32_t)i;
@@ -1343,7 +1269,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
   }
   __syncthreads();
-  DPI_BSTAMP(1);
   const float t = ts;
   // g(x): per-thread dims, then per-statistic block sums in fixed order (one barrier pair)
   {
@@ -1368,7 +1293,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       gx[i] = Eq<KIND>::gfin(e, st);
     }
   }
-  DPI_BSTAMP(2);
   float Cb = 0.f;
   if constexpr (KIND == DPI_EQ_GBM) {
     // exact-solution part of ffi at (t, x) (equations.py:457-466); the NSG dot products w_c . x
@@ -1399,7 +1323,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     }
     const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
     Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
-    DPI_BSTAMP(3);
     if (ZERO) {
       for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
       if (tid == 0) fb[i] = Cb;
@@ -1411,45 +1334,42 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     return;
   }
   const int H = net.H, L = net.L, nxp = net.nxp;
-  // Mat-vecs y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), coalesced in h): thread tid takes
-  // unit h = tid % H and the k-slice tid / H of NTHB / H slices (<= 16 values, all loads issued
-  // before the first FMA: one memory latency per layer); the slices are added in fixed order by
-  // the unit's owner.
-  __shared__ float part[NTHB];
-  [[maybe_unused]] int mv_n = 0;  // stamp variant: the second mat-vec's inner phases (events 11-13)
+  // Mat-vecs y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), H % 16 == 0, coalesced in h): thread
+  // tid takes the 4 units 4 g .. 4 g + 3, g = tid % (H / 4), and the k-slice tid / (H / 4) of
+  // 4096 / H slices (<= 4 k: K <= 4096 / H * 4), one 16-B load per k, all in flight before the first
+  // FMA (a quarter of the load instructions of a unit-per-thread slice: the r05 stamps had the slice
+  // loads at ~22 B/clk into the CU, profiles/r05q_base_stamps_matvec.txt); the wave's slices of a
+  // unit (lanes g + (H / 4) s) are added by lane swaps (their xor tree over s), the 16 waves' partials
+  // in wave order by the unit's owner — a fixed order.
+  __shared__ __attribute__((aligned(16))) float part[NTHB / 64][HMAX];
   auto matvec = [&](const float* __restrict__ Wt, const float* v, int K) -> float {
-#ifdef DPI_BASE_STAMPS
-    const bool mst = mv_n++ == 1;
-    if (mst) DPI_BSTAMP(11);
-#endif
-    const int h = tid % H, ns = NTHB / H, sl = tid / H;
-    const int kc = (K + ns - 1) / ns, k0 = sl * kc, k1 = min(K, k0 + kc);  // kc <= 16
-    float w[16];
+    const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NTHB / G4;
+    const int kc = (K + ns - 1) / ns, k0 = sl * kc;  // kc <= 4
+    float4 w[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = k0 + j < k1 ? Wt[(size_t)(k0 + j) * H + h] : 0.f;  // all loads in flight
-    float a0 = 0.f, a1 = 0.f;
+    for (int j = 0; j < 4; ++j)  // all loads in flight
+      w[j] = (j < kc && k0 + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + j) * H + 4 * g)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 16; j += 2) {
-      if (k0 + j < k1) a0 = fmaf(w[j], v[k0 + j], a0);
-      if (k0 + j + 1 < k1) a1 = fmaf(w[j + 1], v[k0 + j + 1], a1);
-    }
-    part[tid] = a0 + a1;
-#ifdef DPI_BASE_STAMPS
-    if (mst) DPI_BSTAMP(12);
-#endif
+    for (int j = 0; j < 4; ++j)
+      if (j < kc && k0 + j < K) {
+        const float vk = v[k0 + j];
+        a[0] = fmaf(w[j].x, vk, a[0]);
+        a[1] = fmaf(w[j].y, vk, a[1]);
+        a[2] = fmaf(w[j].z, vk, a[2]);
+        a[3] = fmaf(w[j].w, vk, a[3]);
+      }
+    // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
+    for (int o = G4; o < 64; o <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] += __shfl_xor(a[r], o, 64);
+    if ((tid & 63) < G4) *reinterpret_cast<float4*>(&part[tid >> 6][4 * g]) = make_float4(a[0], a[1], a[2], a[3]);
     __syncthreads();
-#ifdef DPI_BASE_STAMPS
-    if (mst) DPI_BSTAMP(13);
-#endif
     float y = 0.f;
     if (tid < H)
-      for (int j = 0; j < ns; ++j) y += part[j * H + tid];
-#ifdef DPI_BASE_STAMPS
-    if (mst) {
-      asm volatile("" ::"v"(y));  // (the stamp waits for y)
-      DPI_BSTAMP(14);
-    }
-#endif
+#pragma unroll
+      for (int j = 0; j < NTHB / 64; ++j) y += part[j][tid];
     return y;  // valid for tid < H; the caller's barrier precedes the next use of part
   };
   // layer 1
@@ -1466,7 +1386,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     if (tid < H) act[l][tid] = act_f(net.act, acc + net.b[l][tid]);
     __syncthreads();
   }
-  DPI_BSTAMP(4);
   if constexpr (KIND == DPI_EQ_GBM) {
     // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
     // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
@@ -1484,7 +1403,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       if (tid < H) lamb[l][tid] = acc;
       __syncthreads();
     }
-    DPI_BSTAMP(5);
     // Tangent sweep as an LDS mat-mat per layer, Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k])
     // Z_{l-1}[k][d]: thread t < 512 owns rows h = hg + 16 j (j < H / 16 <= 4) and columns
     // d = 4 dg .. 4 dg + 3 (hg = t / 32, dg = t % 32), 16 accumulators.  k runs outermost in steps
@@ -1515,7 +1433,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
         }
       }
     }
-    DPI_BSTAMP(6);
     int cz = 0;
     const int H4 = H & ~3;
     for (int l = 1; l < L; ++l) {
@@ -1571,7 +1488,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       }
       cz ^= 1;
       __syncthreads();  // before wsc is overwritten
-      DPI_BSTAMP(6 + l);
     }
     if (sw)
 #pragma unroll
@@ -1583,11 +1499,9 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
     }
     if (tid == 0) fb[i] = Cb;
-    DPI_BSTAMP(10);
     return;
   }
   const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
-  DPI_BSTAMP(5);
   int cur = 0;
   if (tid < H) dbuf[0][tid] = net.wout[tid] * act_d(net.act, act[L - 1][tid]);
   __syncthreads();
@@ -1598,7 +1512,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     cur ^= 1;
     __syncthreads();
   }
-  DPI_BSTAMP(6);
   float gs = 0.f, gA = 0.f, gB = 0.f;
   if (!Eq<KIND>::GRAD_FULL) {
     gs = block_sum_b(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
@@ -1613,7 +1526,6 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     gB = block_sum_b(B, red);
   }
   if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
-  DPI_BSTAMP(10);
 }
 
 struct PathArgs {
@@ -1973,8 +1885,15 @@ __device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, co
 }
 
 // The path launch: one workgroup per (point, 64-path block).
+// Two workgroups per CU (256 registers per wave) except GBM / TD (one: their LDS) and the exact-fp32
+// OU 4 x 128 instance — the range guard's fallback for OU MLP nets — whose GMM statistics beside
+// the 128 fp32 activation registers spilled 4 VGPRs at 256: it runs at one workgroup per CU instead.
+template <int KIND, int H, int L, bool SPLIT, bool TD>
+constexpr int k_paths_wgs() {
+  return (KIND == DPI_EQ_GBM || TD || (KIND == DPI_EQ_OU && !SPLIT && H == 128 && L == 4)) ? 1 : 2;
+}
 template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
-__global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_paths(EqDev e, NetDev net, PathArgs a) {
+__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k_paths(EqDev e, NetDev net, PathArgs a) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, Lds>;
@@ -2007,10 +1926,8 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   }
   const float g_x = a.gx[i], f_b = a.fb[i];
   const float Kf = (float)a.K;
-  constexpr bool STAMP = GBM && !ZERO && !HESS && !TD;
   // GBM prepared calls: phase 1's noise sums come from k_noise_shared (a wave-uniform branch)
   const bool PRE = GBM && !HESS && !TD && a.noise != nullptr;
-  DPI_STAMP(STAMP, 0);
 
   for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
   const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
@@ -2311,12 +2228,9 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   } else if (!tlast) {
     terminal_rollout();
     integral_rollout();
-    DPI_STAMP(STAMP, 1);
     ap = terminal_finish();
-    DPI_STAMP(STAMP, 2);
     integrand();
     __syncthreads();
-    DPI_STAMP(STAMP, 5);
   } else {
     integral_rollout();
     __syncthreads();
@@ -2390,7 +2304,6 @@ __global__ __launch_bounds__(256, (KIND == DPI_EQ_GBM || TD) ? 1 : 2) void k_pat
   } else {
     if (a.tickets) fused_reduce(a, i, F, out);
   }
-  DPI_STAMP(STAMP, 6);
 }
 
 }  // namespace dpi

@@ -139,14 +139,14 @@ class RangeGroup:
             self.gen._release_slot(self.slot)
 
     def __del__(self):
-        # a group dropped unverified gives its slot back; should one of its kernels still flag into
-        # the slot after a later group has taken it, that group merely recomputes in fp32
+        # a group dropped unverified gives its slot back once its kernels are done (an event after
+        # its last call, checked lazily by the next deferred_range_check()): a later group taking the
+        # slot earlier could see this group's flag and recompute its own labels in fp32 for nothing
         try:
             if not self.done:
                 self.done = True
-                if self.gen._scope is self:
-                    self.gen._scope = None
-                self.gen._release_slot(self.slot)
+                self.close()
+                self.gen._release_slot_after(self.slot, self.event)
         except Exception:
             pass
 
@@ -280,6 +280,7 @@ class OnlineDataGenerator:
         self._slot = IMMEDIATE_SLOT
         self._scope = None  # the RangeGroup that label calls are deferred into (deferred_range_check)
         self._free_slots = list(range(UNCHECKED_SLOT - 1, IMMEDIATE_SLOT, -1))
+        self._pending_slots = []  # (slot, event) of groups dropped unverified, until their kernels are done
         self._fp32_fallback = False
         # Points per generator call of the dataset surface (None: unbounded).  The reference sizes
         # its calls by probing GPU memory (picard/memory.py:95-171): a dataset whose calls exceed
@@ -311,6 +312,22 @@ class OnlineDataGenerator:
     def _release_slot(self, slot):
         self._free_slots.append(slot)
 
+    def _release_slot_after(self, slot, event):
+        """`slot` returns to the free list once `event` (the dropped group's last call) completed."""
+        self._pending_slots.append((slot, event))
+
+    def _reclaim_slots(self):
+        """Pending slots whose groups' kernels are done go back to the free list (no wait), or, with
+        no free slot left, the oldest pending one after its event."""
+        keep = []
+        for slot, ev in self._pending_slots:
+            (self._free_slots.append(slot) if ev is None or ev.query() else keep.append((slot, ev)))
+        self._pending_slots = keep
+        if not self._free_slots and self._pending_slots:
+            slot, ev = self._pending_slots.pop(0)
+            ev.synchronize()
+            self._free_slots.append(slot)
+
     def deferred_range_check(self):
         """A RangeGroup that this generator's guarded label calls are deferred into until it is
         closed (use as a context manager, or call close()); verify() it before reading its labels.
@@ -319,6 +336,7 @@ class OnlineDataGenerator:
             return _NoGroup()
         if self._scope is not None:
             raise RuntimeError("deferred_range_check(): a group is already open on this generator")
+        self._reclaim_slots()
         if not self._free_slots:
             raise RuntimeError(f"deferred_range_check(): all {UNCHECKED_SLOT - 1} status slots belong to groups that "
                                "were not verified")

@@ -120,7 +120,10 @@ class IterableDatasetWithInternalBatch(IterableDataset):
     run in one of its RangeGroups, and buffer k is yielded (and saved) only after its group
     verified, which happens once buffer k+1's calls are enqueued — so the check waits on work the
     GPU finished while it already runs the next buffer, instead of synchronising after every call.
-    The buffers are drawn in the same order either way (buffer k+1 is drawn one buffer earlier)."""
+    The buffers are drawn in the same order either way (buffer k+1 is drawn one buffer earlier);
+    an iteration abandoned early (break, islice) discards the buffer drawn ahead unread and rewinds
+    the generator's point counter by its points, so later draws see the counters they would have
+    seen without the guard."""
 
     def __init__(self, n: int, n_batch_buffer: Union[int, float], batch_size: int, batch_data_generator,
                  range_guard=None):
@@ -179,23 +182,27 @@ class IterableDatasetWithInternalBatch(IterableDataset):
             for _ in range(self.n_buffer_refresh):
                 yield from self._emit(*self.refresh_buffer())
         else:
-            pending = None  # (group, xs, ys) of the buffer drawn but not yet verified
+            pending = None  # (group, xs, ys, point counter before its draws) of the buffer drawn, not yet verified
+            gen = self.range_guard
             try:
                 for _ in range(self.n_buffer_refresh):
-                    with self.range_guard.deferred_range_check() as grp:
+                    pb0 = getattr(gen, "point_base", None)
+                    with gen.deferred_range_check() as grp:
                         xs, ys = self._calls()
-                    if pending is not None:
-                        (g, pxs, pys), pending = pending, None
+                    prev, pending = pending, (grp, xs, ys, pb0)
+                    if prev is not None:
+                        g, pxs, pys, _ = prev
                         g.verify()  # joined after the check: a repair writes the calls' own outputs
                         yield from self._emit(*self._joined(pxs, pys))
-                    pending = (grp, xs, ys)
                 if pending is not None:
-                    (g, pxs, pys), pending = pending, None
+                    (g, pxs, pys, _), pending = pending, None
                     g.verify()
                     yield from self._emit(*self._joined(pxs, pys))
             finally:
                 if pending is not None:  # iteration abandoned: the drawn buffer is dropped unread
                     pending[0].discard()
+                    if pending[3] is not None:  # and its points' counters handed back
+                        gen.point_base = pending[3]
         if self.saver is not None:
             self.saver.close()
 

@@ -56,6 +56,58 @@ def test_batches_come_out_in_draw_order(nbuf):
     assert gen.calls == ([24] * 4 if nbuf == 3 else [2] * 48)
 
 
+class _GuardedCounting(CountingGenerator):
+    """CountingGenerator with the range-guard surface the dataset uses: a point counter (the
+    generator's point_base) and deferred_range_check() groups that record verify / discard."""
+
+    class _Group:
+        def __init__(self, log):
+            self.log = log
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+        def verify(self):
+            self.log.append("verify")
+            return 0
+
+        def discard(self):
+            self.log.append("discard")
+
+    def __init__(self):
+        super().__init__()
+        self.log = []
+
+    @property
+    def point_base(self):
+        return self.next
+
+    @point_base.setter
+    def point_base(self, v):
+        self.next = v
+
+    def deferred_range_check(self):
+        return self._Group(self.log)
+
+
+def test_guarded_dataset_abandoned_early_rewinds_the_drawn_ahead_buffer():
+    """with a range guard the dataset draws buffer k+1 before it yields buffer k; a
+    consumer that stops early leaves that buffer unread — it is discarded and the generator's point
+    counter handed back, so the next draw starts where an unguarded dataset's would."""
+    import itertools
+    gen = _GuardedCounting()
+    ds = D.IterableDatasetWithInternalBatch(96, 2, 8, gen, range_guard=gen)  # 6 buffers of 16 points
+    got = list(itertools.islice(iter(ds), 3))  # buffer 0 and half of buffer 1
+    assert torch.equal(torch.cat([b[0] for b in got])[:, 0], torch.arange(24, dtype=torch.float64))
+    assert gen.point_base == 32 and gen.log[-1] == "discard"  # buffer 2 (points 32-47) drawn ahead, given back
+    full = list(ds)  # a complete pass afterwards continues at 32, every buffer verified
+    assert torch.equal(torch.cat([b[0] for b in full])[:, 0], torch.arange(32, 128, dtype=torch.float64))
+    assert gen.log.count("verify") == 2 + 6
+
+
 def test_size_must_be_a_multiple_of_the_buffer():
     with pytest.raises(AssertionError):
         D.IterableDatasetWithInternalBatch(100, 3, 8, CountingGenerator())

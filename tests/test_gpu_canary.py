@@ -82,7 +82,7 @@ def _stream():
 
 def _first_order(gen, n, M, m0, m1, flags=L.DPI_BOTH, finalize=True, prepared=False):
     F = 1 + NX
-    need = gen.workspace_bytes(n, M)
+    need = gen.workspace_bytes(n, M, prepared=prepared)  # prepared: + the staged noise sums (GBM)
     c = Carved(ws=need, mom=n * 2 * F * 4, y=n * F * 4)
     tx, pb = gen.sample_t_and_x(n, point_base=11)
     gen.point_baseline(tx, ws=c.u8("ws"))
@@ -141,11 +141,13 @@ def test_first_order_calls_write_nothing_outside_their_buffers(case, mode):
     _first_order(gen, n, M, m0, m1, flags, fin, prep)
 
 
-@pytest.mark.parametrize("n,M,m0,m1", [(3, 192, 0, 192), (5, 256, 64, 192), (2, 8192, 0, 8192)])
-def test_hessian_label_calls_write_nothing_outside_their_buffers(n, M, m0, m1):
-    """dpi_label_moments_hessians + dpi_label_finalize_hessians (a shard with m_begin > 0, and more
-    than 64 path blocks: the wave-per-column reduce), and the one-call
-    dpi_generate_with_gradients_and_hessians."""
+@pytest.mark.parametrize("n,M,m0,m1,flags", [(3, 192, 0, 192, L.DPI_BOTH), (5, 256, 64, 192, L.DPI_BOTH),
+                                             (2, 8192, 0, 8192, L.DPI_BOTH), (3, 128, 0, 128, L.DPI_TERMINAL),
+                                             (3, 192, 64, 192, L.DPI_INTEGRAL)])
+def test_hessian_label_calls_write_nothing_outside_their_buffers(n, M, m0, m1, flags):
+    """dpi_label_moments_hessians + dpi_label_finalize_hessians (a shard with m_begin > 0, more than
+    64 path blocks: the wave-per-column reduce, one estimator alone: the unequal-count passes), and
+    the one-call dpi_generate_with_gradients_and_hessians."""
     gen = _gen("gbm", M)
     F, C = 1 + NX, NX * NX
     need = max(gen.workspace_bytes(n, M, hessians=True), gen.workspace_bytes(n, M))
@@ -154,17 +156,18 @@ def test_hessian_label_calls_write_nothing_outside_their_buffers(n, M, m0, m1):
     gen.point_baseline(tx, hessians=True, ws=c.u8("ws"))
     lib, p, h = gen.lib, gen.problem, gen.net.handle
     txp = ctypes.c_void_p(tx.data_ptr())
-    L.check(lib.dpi_label_moments_hessians(p, h, txp, n, M, gen.K, gen.seed, gen.epoch, pb, m0, m1, c.ptr("mom"),
-                                           c.ptr("hs"), c.ptr("ws"), c.nbytes("ws"), _stream()), "moments_hessians")
-    L.check(lib.dpi_label_finalize_hessians(p, c.ptr("mom"), c.ptr("hs"), n, M, float("inf"), c.ptr("y"), c.ptr("ws"),
-                                            c.nbytes("ws"), _stream()), "finalize_hessians")
-    if (m0, m1) == (0, M):
+    L.check(lib.dpi_label_moments_hessians(p, h, txp, n, M, gen.K, gen.seed, gen.epoch, pb, m0, m1, flags,
+                                           c.ptr("mom"), c.ptr("hs"), c.ptr("ws"), c.nbytes("ws"), _stream()),
+            "moments_hessians")
+    L.check(lib.dpi_label_finalize_hessians(p, c.ptr("mom"), c.ptr("hs"), n, M, flags, float("inf"), c.ptr("y"),
+                                            c.ptr("ws"), c.nbytes("ws"), _stream()), "finalize_hessians")
+    if (m0, m1) == (0, M) and flags == L.DPI_BOTH:
         L.check(lib.dpi_generate_with_gradients_and_hessians(p, h, txp, n, M, gen.K, gen.seed, gen.epoch, pb,
                                                              float("inf"), c.ptr("y1"), c.ptr("ws"), c.nbytes("ws"),
                                                              _stream()), "generate_hessians")
     c.check()
     assert torch.isfinite(c.f32("y", n, F + C)).all()
-    if (m0, m1) == (0, M):
+    if (m0, m1) == (0, M) and flags == L.DPI_BOTH:
         assert torch.equal(c.f32("y", n, F + C), c.f32("y1", n, F + C))
 
 
