@@ -1,7 +1,9 @@
 #!/bin/bash
-# One GPU call of a round: GPU tests, bench lines for every workload, kernel traces (one stream for
-# HJB), the counter list and the VALU / HBM PMC passes of the Burgers bench.
-# usage: tools/gpu_round.sh <tag> [tests|bench|trace|pmc ...]   outputs under gpurun_out/<tag>/
+# One GPU call of a round, by stages: GPU tests, bench lines for every workload, kernel traces (one
+# stream for HJB), the counter list, the VALU / HBM PMC passes, same-box A/B against the round-5
+# package (ab, probe: tools/variants/r05pkg), the N = 2 gloo rehearsals and the RCCL smoke.
+# usage: tools/gpu_round.sh <tag> [tests|bench|trace|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
+#        outputs under gpurun_out/<tag>/
 set -e
 tag=${1:-r02}; shift || true
 what=${*:-tests bench trace pmc}
@@ -33,6 +35,15 @@ for w in $what; do
   hjbprep)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_prepare -o trace --output-format csv -- \
       python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_hjb_prepare.log 2>&1 ;;
+  ab)
+    tools/ab_bench.sh $tag/ab burgers hjb gbm gbm_hess ;;
+  probe)
+    tools/ab_probe_small.sh $tag/probe_small "" homog,all ;;
+  rehearsal)
+    tools/rehearsal_n2.sh $tag ;;
+  nccl)
+    run 180 $out/nccl_smoke.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+      --master-port 29511 tools/nccl_smoke.py ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
   pmc)
