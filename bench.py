@@ -25,6 +25,7 @@ all-reduce — is the code the RCCL run executes.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 from pathlib import Path
@@ -48,7 +49,7 @@ PEAK_CLOCK_GHZ = 2.4   # MI355X peak engine clock (MI355X_MICROARCH.md)
 # "peak": the MFMA the kernel's network evaluation runs on.
 WORKLOADS = {
     "burgers": dict(cfg="configs[1]", eq="Cha", widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0,
-                    flop=2.72e5, peak="split", kernel="k_paths<Cha,128,4,split> + k_reduce per dpi_label_moments call", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
+                    flop=2.72e5, peak="split", kernel="k_paths_fb<Cha,128,4,split>: per-point baseline, rollouts, network and label reduce in one launch per sample_with_gradients call (N > 1: k_baseline + k_paths<Cha,128,4,split>)", desc="Burgers 100d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
                                       "MLP 101-128x4-1 ELU (BASELINE configs[1]; N>1: MC-sharded, configs[3] pattern)"),
     "burgers_cfg3": dict(cfg="configs[3]", eq="Cha", widths=[128] * 4, points=512, m_total=4096, K=50, sdgd=0,
                          flop=2.72e5, peak="split", scaling="strong",
@@ -505,8 +506,9 @@ def main():
         if vf.exists() and not wl.get("pis"):
             kern = json.loads(vf.read_text())["kernels"]
             # k_paths<KIND, H, L, ZERO, SPLIT, HESS, TD, ACT>: the network launch, not the u = 0 twin
+            # (k_paths_fb<KIND, H, L, ZERO, SPLIT, ACT>: the one-launch sample_with_gradients, base blocks included)
             net_k = [v for k, v in kern.items()
-                     if "k_paths<" in k and k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
+                     if re.search(r"k_paths(_fb)?<", k) and k.split("<", 1)[1].rstrip(">").split(", ")[3] != "true"]
             top = max(net_k, key=lambda v: v["dispatches"])
             busy = top["valu_busy_cycles_per_simd"] * scale
             # the GBM prepare schedule: the next batch's noise sums (k_noise_shared, prepare stream) issue

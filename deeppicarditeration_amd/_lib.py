@@ -10,7 +10,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("DPI_HIP_LIB", _HERE / "libdpi_hip.so"))
 
 # constants mirrored from include/dpi.h (checked against the header by tests/test_capi.py)
-DPI_ABI_VERSION = 4
+DPI_ABI_VERSION = 5
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
 DPI_EQ_CHA, DPI_EQ_OU, DPI_EQ_GBM = 1, 2, 3
@@ -21,6 +21,7 @@ DPI_PATH_BLOCK = 64
 DPI_PATHS_PER_CALL_MAX = 1024 * DPI_PATH_BLOCK
 DPI_GEMM_F32, DPI_GEMM_F16X3, DPI_GEMM_AUTO = 0, 1, 2
 DPI_STATUS_NONFINITE = 1
+DPI_STATUS_HANDOFF = 2
 DPI_STATUS_SLOTS = 64
 
 c_int, c_double, c_float, c_size_t, c_void_p, c_uint32, c_uint64 = (

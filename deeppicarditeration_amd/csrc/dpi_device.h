@@ -1211,34 +1211,231 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-constexpr int NTHB = 1024;  // baseline workgroup: 16 waves
-__device__ __forceinline__ float block_sum_b(float v, float* red) {
+constexpr int NTHB = 1024;  // GBM baseline workgroup: 16 waves (the Hessian-diagonal sweep)
+constexpr int NTB = 256;    // Cha / OU baseline workgroup: k_baseline, and k_paths' fused base blocks
+// Block-wide sum over NT threads in wave order (result on every thread); red: >= NT / 64 floats of LDS.
+template <int NT>
+__device__ __forceinline__ float block_sum_n(float v, float* red) {
   v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   float a = 0.f;
-  for (int w = 0; w < NTHB / 64; ++w) a += red[w];
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) a += red[w];
   return a;
 }
 
-// Baseline per point (one workgroup per point): g(x), the state-dependent part of
-// f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920 g_single, :506-518
-// f_baseline).  A latency-bound handful of points: 1024 threads per point split every mat-vec
-// over k-slices (weights read coalesced through the transposed copies), no LDS staging.
-// smp.tx != null: the block first samples its point (draws 1-3, k_sample_points' arithmetic) into
-// smp.tx and its LDS copy, so sample_with_gradients needs no sampling launch; tickets != null: zero
-// this point's ticket of the fused label reduce (k_paths' last-block reduce).
+// Mat-vec of the per-point baseline, y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), H in {16, 32,
+// 64, 128}, coalesced in h), over a block of NT threads: thread tid takes the 4 units 4 g .. 4 g + 3,
+// g = tid % (H / 4), and the k-slice tid / (H / 4) of NT / (H / 4) slices (<= 4096 / NT k per slice),
+// one 16-B load per k, all in flight before the first FMA (the r05 stamps had unit-per-thread slice
+// loads at ~22 B/clk into the CU, profiles/r05q_base_stamps_matvec.txt); the wave's slices of a unit
+// (lanes g + (H / 4) s) are added by lane swaps (their xor tree over s), the waves' partials in wave
+// order by the unit's owner — a fixed order.  Returns y[tid] for tid < H; the caller's barrier
+// precedes the next use of part.
+template <int NT>
+__device__ __forceinline__ float base_matvec(const float* __restrict__ Wt, const float* v, int K, int H,
+                                             float (*part)[HMAX]) {
+  constexpr int KCM = HMAX * HMAX / 4 / NT;  // max k per slice
+  const int tid = threadIdx.x;
+  const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NT / G4;
+  const int kc = (K + ns - 1) / ns, k0 = sl * kc;
+  float4 w[KCM];
+#pragma unroll
+  for (int j = 0; j < KCM; ++j)  // all loads in flight
+    w[j] = (j < kc && k0 + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + j) * H + 4 * g)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < KCM; ++j)
+    if (j < kc && k0 + j < K) {
+      const float vk = v[k0 + j];
+      a[0] = fmaf(w[j].x, vk, a[0]);
+      a[1] = fmaf(w[j].y, vk, a[1]);
+      a[2] = fmaf(w[j].z, vk, a[2]);
+      a[3] = fmaf(w[j].w, vk, a[3]);
+    }
+  // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
+  for (int o = G4; o < 64; o <<= 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] += __shfl_xor(a[r], o, 64);
+  if ((tid & 63) < G4) *reinterpret_cast<float4*>(&part[tid >> 6][4 * g]) = make_float4(a[0], a[1], a[2], a[3]);
+  __syncthreads();
+  float y = 0.f;
+  if (tid < H)
+#pragma unroll
+    for (int j = 0; j < NT / 64; ++j) y += part[j][tid];
+  return y;
+}
+
+// Per-point baseline scratch: k_baseline's LDS, and an overlay of the path LDS in k_paths' fused
+// base blocks (a workgroup runs one role).
+template <int NT>
+struct BaseLds {
+  __attribute__((aligned(16))) float part[NT / 64][HMAX];
+  float xs[NXP_MAX];
+  float act[4][HMAX];
+  float dbuf[2][HMAX];
+  float red[NT / 64];
+  float redn[NT / 64][NSG];
+  float ts;
+};
+
+// The fused launch's per-point baseline record: [g(x), f_b, pad to 32][bx: HMAX], 640 B, so no
+// 128-B line holds values of two points (each point's values are handed off on their own).
+constexpr int BREC = 32 + HMAX;
+
+// Baseline of point i over a block of NT threads (Cha / OU; GBM: k_baseline_gbm): g(x), the
+// state-dependent part of f(t, x, u, grad u) and bx = b1 + W1[:,1:] x (picard/data.py:918-920
+// g_single, :506-518 f_baseline).  A latency-bound chain of block-wide mat-vecs (weights read
+// coalesced through the transposed copies).  smp.tx != null: the block first samples its point
+// (draws 1-3, k_sample_points' arithmetic) into smp.tx and its LDS copy; tickets != null: zero the
+// point's ticket of the fused label reduce; rec != null: the values also go to the point's record.
+template <int KIND, bool ZERO, int NT>
+__device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, const float* __restrict__ tx, int i,
+                                           float* __restrict__ gx, float* __restrict__ fb, float* __restrict__ bx,
+                                           float* __restrict__ rec, const SampleSpec& smp, int* __restrict__ tickets,
+                                           BaseLds<NT>& bs) {
+  static_assert(KIND != DPI_EQ_GBM, "GBM: k_baseline_gbm");
+  static_assert(NT >= NXP_MAX && NT % 64 == 0, "one thread per padded state dimension");
+  const int tid = threadIdx.x;
+  const int nx = e.nx, F = 1 + nx;
+  float* const r = rec ? rec + (size_t)i * BREC : nullptr;
+  if (tickets && tid == 0) tickets[i] = 0;
+  if (smp.tx) {
+    const uint32_t ig = smp.point_base + (uint32_t)i;
+    const int nb = (nx + 3) >> 2;
+    float* row = smp.tx + (size_t)i * F;
+    if (tid < nb) {
+      const float tt = sample_point_t(e, smp, ig);
+      if (tid == 0) {
+        row[0] = tt;
+        bs.ts = tt;
+      }
+      float x[4];
+      sample_point_x4<KIND>(e, smp, ig, tid, tt, x);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * tid + q;
+        if (d < nx) row[1 + d] = x[q];
+        bs.xs[d] = d < nx ? x[q] : 0.f;
+      }
+    } else if (4 * nb <= tid && tid < NXP_MAX) {
+      bs.xs[tid] = 0.f;
+    }
+  } else {
+    const float* row = tx + (size_t)i * F;
+    if (tid == 0) bs.ts = row[0];
+    if (tid < NXP_MAX) bs.xs[tid] = tid < nx ? row[1 + tid] : 0.f;
+  }
+  __syncthreads();
+  const float t = bs.ts;
+  // g(x): per-thread dims, then per-statistic block sums in wave order (one barrier pair)
+  {
+    float st[NSG];
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = 0.f;
+    for (int d = tid; d < nx; d += NT) Eq<KIND>::gstat(e, d, bs.xs[d], st);
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) st[c] = wave_sum(st[c]);
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) bs.redn[tid >> 6][c] = st[c];
+    __syncthreads();
+    if (tid == 0) {
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) {
+        float a = 0.f;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) a += bs.redn[w][c];
+        st[c] = a;
+      }
+      const float g = Eq<KIND>::gfin(e, st);
+      gx[i] = g;
+      if (r) r[0] = g;
+    }
+  }
+  if (ZERO) {
+    if (tid == 0) {
+      const float f = Eq<KIND>::ffv(e, 0.f, 0.f, 0.f, 0.f);
+      fb[i] = f;
+      if (r) r[1] = f;
+    }
+    return;
+  }
+  const int H = net.H, L = net.L, nxp = net.nxp;
+  // layer 1
+  {
+    const float acc = base_matvec<NT>(net.W1xT, bs.xs, nx, H, bs.part);
+    if (tid < H) {
+      const float v = net.b1[tid] + acc;
+      bx[(size_t)i * H + tid] = v;
+      if (r) r[32 + tid] = v;
+      bs.act[0][tid] = act_f(net.act, fmaf(net.w1t[tid], t, v));
+    }
+    __syncthreads();
+  }
+  for (int l = 1; l < L; ++l) {
+    const float acc = base_matvec<NT>(net.WT[l], bs.act[l - 1], H, H, bs.part);
+    if (tid < H) bs.act[l][tid] = act_f(net.act, acc + net.b[l][tid]);
+    __syncthreads();
+  }
+  const float u = block_sum_n<NT>(tid < H ? net.wout[tid] * bs.act[L - 1][tid] : 0.f, bs.red) + net.bout;
+  int cur = 0;
+  if (tid < H) bs.dbuf[0][tid] = net.wout[tid] * act_d(net.act, bs.act[L - 1][tid]);
+  __syncthreads();
+  for (int l = L - 2; l >= 0; --l) {
+    // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
+    const float acc = base_matvec<NT>(net.W[l + 1], bs.dbuf[cur], H, H, bs.part);
+    if (tid < H) bs.dbuf[cur ^ 1][tid] = acc * act_d(net.act, bs.act[l][tid]);
+    cur ^= 1;
+    __syncthreads();
+  }
+  float gs = 0.f, gA = 0.f, gB = 0.f;
+  if (!Eq<KIND>::GRAD_FULL) {
+    gs = block_sum_n<NT>(tid < H ? net.c1[tid] * bs.dbuf[cur][tid] : 0.f, bs.red);
+  } else {
+    float A = 0.f, B = 0.f;
+    for (int d = tid; d < nx; d += NT) {
+      float z = 0.f;
+      for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], bs.dbuf[cur][k], z);
+      Eq<KIND>::gacc(e, d, bs.xs[d], z, A, B);
+    }
+    gA = block_sum_n<NT>(A, bs.red);
+    gB = block_sum_n<NT>(B, bs.red);
+  }
+  if (tid == 0) {
+    const float f = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
+    fb[i] = f;
+    if (r) r[1] = f;
+  }
+}
+
+// Per-point baseline launch (Cha / OU): one NTB-thread workgroup per point.
 template <int KIND, bool ZERO>
-__global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
-                                                  float* __restrict__ gx, float* __restrict__ fb,
-                                                  float* __restrict__ bx, float* __restrict__ hb, SampleSpec smp,
-                                                  int* __restrict__ tickets) {
+__global__ __launch_bounds__(NTB) void k_baseline(EqDev e, NetDev net, const float* __restrict__ tx, int n,
+                                                 float* __restrict__ gx, float* __restrict__ fb,
+                                                 float* __restrict__ bx, SampleSpec smp, int* __restrict__ tickets) {
+  __shared__ BaseLds<NTB> bs;
+  (void)n;
+  base_point<KIND, ZERO, NTB>(e, net, tx, blockIdx.x, gx, fb, bx, nullptr, smp, tickets, bs);
+}
+
+// GBM per-point baseline (one 1024-thread workgroup per point): g(x), the exact-solution part of
+// ffi at (t, x) (equations.py:457-466), bx = b1 + W1[:,1:] x and the network's Hessian diagonal at
+// (t, x) for the SDGD baseline gather (data.py:1293-1302).  smp / tickets as base_point.
+template <bool ZERO>
+__global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, const float* __restrict__ tx, int n,
+                                                      float* __restrict__ gx, float* __restrict__ fb,
+                                                      float* __restrict__ bx, float* __restrict__ hb, SampleSpec smp,
+                                                      int* __restrict__ tickets) {
+  constexpr int KIND = DPI_EQ_GBM;
   __shared__ float xs[NXP_MAX];
   __shared__ float act[4][HMAX];
-  __shared__ float dbuf[2][HMAX];
   __shared__ float red[NTHB / 64];
   __shared__ float ts;
+  (void)n;
   const int i = blockIdx.x, tid = threadIdx.x;
   const int nx = e.nx, F = 1 + nx;
   if (tickets && tid == 0) tickets[i] = 0;
@@ -1293,88 +1490,44 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
       gx[i] = Eq<KIND>::gfin(e, st);
     }
   }
-  float Cb = 0.f;
-  if constexpr (KIND == DPI_EQ_GBM) {
-    // exact-solution part of ffi at (t, x) (equations.py:457-466); the NSG dot products w_c . x
-    // reduced together (one barrier pair instead of one per component, each sum in block_sum_b's order)
-    float arg[NSG], sn[NSG];
-    {
-      __shared__ float redw[NTHB / 64][NSG];
-      float v[NSG];
+  // exact-solution part of ffi at (t, x) (equations.py:457-466); the NSG dot products w_c . x
+  // reduced together (one barrier pair instead of one per component, each sum in block_sum_n's order)
+  float arg[NSG], sn[NSG];
+  {
+    __shared__ float redw[NTHB / 64][NSG];
+    float v[NSG];
 #pragma unroll
-      for (int c = 0; c < NSG; ++c) {
-        v[c] = 0.f;
-        if (c < e.nodes)
-          for (int d = tid; d < nx; d += NTHB) v[c] = fmaf(e.gw[c * F + 1 + d], xs[d], v[c]);
-        v[c] = wave_sum(v[c]);
-      }
-      __syncthreads();
-      if ((tid & 63) == 0)
-#pragma unroll
-        for (int c = 0; c < NSG; ++c) redw[tid >> 6][c] = v[c];
-      __syncthreads();
-#pragma unroll
-      for (int c = 0; c < NSG; ++c) {
-        float a = 0.f;
-        for (int w = 0; w < NTHB / 64; ++w) a += redw[w][c];
-        arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, a) : 0.f;
-        sn[c] = __sinf(arg[c]);
-      }
+    for (int c = 0; c < NSG; ++c) {
+      v[c] = 0.f;
+      if (c < e.nodes)
+        for (int d = tid; d < nx; d += NTHB) v[c] = fmaf(e.gw[c * F + 1 + d], xs[d], v[c]);
+      v[c] = wave_sum(v[c]);
     }
-    const float ah = block_sum_b(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
-    Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
-    if (ZERO) {
-      for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
-      if (tid == 0) fb[i] = Cb;
-      return;
+    __syncthreads();
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int c = 0; c < NSG; ++c) redw[tid >> 6][c] = v[c];
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NSG; ++c) {
+      float a = 0.f;
+      for (int w = 0; w < NTHB / 64; ++w) a += redw[w][c];
+      arg[c] = c < e.nodes ? fmaf(e.gw[c * F], t, a) : 0.f;
+      sn[c] = __sinf(arg[c]);
     }
   }
+  const float ah = block_sum_n<NTHB>(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
+  const float Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
   if (ZERO) {
-    if (tid == 0) fb[i] = Eq<KIND>::ffv(e, 0.f, 0.f, 0.f, 0.f);
+    for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
+    if (tid == 0) fb[i] = Cb;
     return;
   }
   const int H = net.H, L = net.L, nxp = net.nxp;
-  // Mat-vecs y[h] = sum_k Wt[k][h] v[k] (Wt row-major (K, H), H % 16 == 0, coalesced in h): thread
-  // tid takes the 4 units 4 g .. 4 g + 3, g = tid % (H / 4), and the k-slice tid / (H / 4) of
-  // 4096 / H slices (<= 4 k: K <= 4096 / H * 4), one 16-B load per k, all in flight before the first
-  // FMA (a quarter of the load instructions of a unit-per-thread slice: the r05 stamps had the slice
-  // loads at ~22 B/clk into the CU, profiles/r05q_base_stamps_matvec.txt); the wave's slices of a
-  // unit (lanes g + (H / 4) s) are added by lane swaps (their xor tree over s), the 16 waves' partials
-  // in wave order by the unit's owner — a fixed order.
   __shared__ __attribute__((aligned(16))) float part[NTHB / 64][HMAX];
-  auto matvec = [&](const float* __restrict__ Wt, const float* v, int K) -> float {
-    const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NTHB / G4;
-    const int kc = (K + ns - 1) / ns, k0 = sl * kc;  // kc <= 4
-    float4 w[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)  // all loads in flight
-      w[j] = (j < kc && k0 + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + j) * H + 4 * g)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j < kc && k0 + j < K) {
-        const float vk = v[k0 + j];
-        a[0] = fmaf(w[j].x, vk, a[0]);
-        a[1] = fmaf(w[j].y, vk, a[1]);
-        a[2] = fmaf(w[j].z, vk, a[2]);
-        a[3] = fmaf(w[j].w, vk, a[3]);
-      }
-    // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
-    for (int o = G4; o < 64; o <<= 1)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] += __shfl_xor(a[r], o, 64);
-    if ((tid & 63) < G4) *reinterpret_cast<float4*>(&part[tid >> 6][4 * g]) = make_float4(a[0], a[1], a[2], a[3]);
-    __syncthreads();
-    float y = 0.f;
-    if (tid < H)
-#pragma unroll
-      for (int j = 0; j < NTHB / 64; ++j) y += part[j][tid];
-    return y;  // valid for tid < H; the caller's barrier precedes the next use of part
-  };
   // layer 1
   {
-    const float acc = matvec(net.W1xT, xs, nx);
+    const float acc = base_matvec<NTHB>(net.W1xT, xs, nx, H, part);
     if (tid < H) {
       bx[(size_t)i * H + tid] = net.b1[tid] + acc;
       act[0][tid] = act_f(net.act, fmaf(net.w1t[tid], t, net.b1[tid] + acc));
@@ -1382,150 +1535,118 @@ __global__ __launch_bounds__(NTHB) void k_baseline(EqDev e, NetDev net, const fl
     __syncthreads();
   }
   for (int l = 1; l < L; ++l) {
-    const float acc = matvec(net.WT[l], act[l - 1], H);
+    const float acc = base_matvec<NTHB>(net.WT[l], act[l - 1], H, H, part);
     if (tid < H) act[l][tid] = act_f(net.act, acc + net.b[l][tid]);
     __syncthreads();
   }
-  if constexpr (KIND == DPI_EQ_GBM) {
-    // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
-    // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
-    __shared__ float lamb[4][HMAX];
-    __shared__ float cb[HMAX];
-    __shared__ __attribute__((aligned(16))) float ztb[2][64][NXP_MAX];
-    if (tid < H) lamb[L - 1][tid] = net.wout[tid];
+  // Hessian diagonal at (t, x): adjoints lam_l = du/da_l, then one thread per state dimension
+  // runs its first-order tangent chain (column-major in LDS) and contracts with lam_l * elu''.
+  __shared__ float lamb[4][HMAX];
+  __shared__ float cb[HMAX];
+  __shared__ __attribute__((aligned(16))) float ztb[2][64][NXP_MAX];
+  if (tid < H) lamb[L - 1][tid] = net.wout[tid];
+  __syncthreads();
+  // adjoints: lam_l = W_{l+1}^T (elu'(a_{l+1}) * lam_{l+1}), a k-sliced mat-vec over the block with
+  // every weight load in flight (W_{l+1} row-major (H_out, H_in) is its transposed operand)
+  for (int l = L - 2; l >= 0; --l) {
+    if (tid < H) cb[tid] = act_d(net.act, act[l + 1][tid]) * lamb[l + 1][tid];
     __syncthreads();
-    // adjoints: lam_l = W_{l+1}^T (elu'(a_{l+1}) * lam_{l+1}), a k-sliced mat-vec over the block with
-    // every weight load in flight (W_{l+1} row-major (H_out, H_in) is its transposed operand)
-    for (int l = L - 2; l >= 0; --l) {
-      if (tid < H) cb[tid] = act_d(net.act, act[l + 1][tid]) * lamb[l + 1][tid];
-      __syncthreads();
-      const float acc = matvec(net.W[l + 1], cb, H);
-      if (tid < H) lamb[l][tid] = acc;
-      __syncthreads();
+    const float acc = base_matvec<NTHB>(net.W[l + 1], cb, H, H, part);
+    if (tid < H) lamb[l][tid] = acc;
+    __syncthreads();
+  }
+  // Tangent sweep as an LDS mat-mat per layer, Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k])
+  // Z_{l-1}[k][d]: thread t < 512 owns rows h = hg + 16 j (j < H / 16 <= 4) and columns
+  // d = 4 dg .. 4 dg + 3 (hg = t / 32, dg = t % 32), 16 accumulators.  k runs outermost in steps
+  // of 4: per step one float4 of Z per k and one broadcast float4 of scaled weights per row, a
+  // third of the LDS return bytes of the column-per-thread form, which was bound by them (2.4 MB
+  // per layer; 22 K cycles of the launch's 87 K, tools/base_stamps.py r05j).  Every output is the
+  // same k-ascending fma chain as before; only the row grouping of the u_dd partials changed.
+  __shared__ __attribute__((aligned(16))) float wsc[64 * 64];
+  __shared__ float udp[16][NXP_MAX];
+  const bool sw = tid < 512;
+  const int dg = tid & 31, hg = (tid >> 5) & 15, RJ = (H + 15) >> 4;
+  float ud[4] = {0.f, 0.f, 0.f, 0.f};
+  if (sw) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int h = hg + 16 * j;
+      if (j < RJ && h < H) {
+        float z[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * dg + q;
+          z[q] = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
+        }
+        *reinterpret_cast<float4*>(&ztb[0][h][4 * dg]) = make_float4(z[0], z[1], z[2], z[3]);
+        const float c = lamb[0][h] * act_d2(net.act, act[0][h]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[q] * z[q], ud[q]);
+      }
     }
-    // Tangent sweep as an LDS mat-mat per layer, Z_l[h][d] = sum_k W_l[h][k] elu'(a_{l-1}[k])
-    // Z_{l-1}[k][d]: thread t < 512 owns rows h = hg + 16 j (j < H / 16 <= 4) and columns
-    // d = 4 dg .. 4 dg + 3 (hg = t / 32, dg = t % 32), 16 accumulators.  k runs outermost in steps
-    // of 4: per step one float4 of Z per k and one broadcast float4 of scaled weights per row, a
-    // third of the LDS return bytes of the column-per-thread form, which was bound by them (2.4 MB
-    // per layer; 22 K cycles of the launch's 87 K, tools/base_stamps.py r05j).  Every output is the
-    // same k-ascending fma chain as before; only the row grouping of the u_dd partials changed.
-    __shared__ __attribute__((aligned(16))) float wsc[64 * 64];
-    __shared__ float udp[16][NXP_MAX];
-    const bool sw = tid < 512;
-    const int dg = tid & 31, hg = (tid >> 5) & 15, RJ = (H + 15) >> 4;
-    float ud[4] = {0.f, 0.f, 0.f, 0.f};
+  }
+  int cz = 0;
+  const int H4 = H & ~3;
+  for (int l = 1; l < L; ++l) {
+    for (int q = tid; q < H * H; q += NTHB) {
+      const int h = q / H, k = q - h * H;
+      wsc[h * 64 + k] = net.W[l][q] * act_d(net.act, act[l - 1][k]);
+    }
+    __syncthreads();  // wsc and Z_{l-1} complete
     if (sw) {
+      float z[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[j][q] = 0.f;
+#pragma unroll 1
+      for (int k = 0; k < H4; k += 4) {
+        const float4 z0 = *reinterpret_cast<const float4*>(&ztb[cz][k][4 * dg]);
+        const float4 z1 = *reinterpret_cast<const float4*>(&ztb[cz][k + 1][4 * dg]);
+        const float4 z2 = *reinterpret_cast<const float4*>(&ztb[cz][k + 2][4 * dg]);
+        const float4 z3 = *reinterpret_cast<const float4*>(&ztb[cz][k + 3][4 * dg]);
+        const float a0[4] = {z0.x, z0.y, z0.z, z0.w}, a1[4] = {z1.x, z1.y, z1.z, z1.w};
+        const float a2[4] = {z2.x, z2.y, z2.z, z2.w}, a3[4] = {z3.x, z3.y, z3.z, z3.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < RJ && hg + 16 * j < H) {
+            const float4 w = *reinterpret_cast<const float4*>(&wsc[(hg + 16 * j) * 64 + k]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              z[j][q] = fmaf(w.w, a3[q], fmaf(w.z, a2[q], fmaf(w.y, a1[q], fmaf(w.x, a0[q], z[j][q]))));
+          }
+      }
+      for (int k = H4; k < H; ++k) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j < RJ && hg + 16 * j < H)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[j][q] = fmaf(wsc[(hg + 16 * j) * 64 + k], ztb[cz][k][4 * dg + q], z[j][q]);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int h = hg + 16 * j;
         if (j < RJ && h < H) {
-          float z[4];
+          *reinterpret_cast<float4*>(&ztb[cz ^ 1][h][4 * dg]) = make_float4(z[j][0], z[j][1], z[j][2], z[j][3]);
+          const float c = lamb[l][h] * act_d2(net.act, act[l][h]);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int d = 4 * dg + q;
-            z[q] = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
-          }
-          *reinterpret_cast<float4*>(&ztb[0][h][4 * dg]) = make_float4(z[0], z[1], z[2], z[3]);
-          const float c = lamb[0][h] * act_d2(net.act, act[0][h]);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[q] * z[q], ud[q]);
+          for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[j][q] * z[j][q], ud[q]);
         }
       }
     }
-    int cz = 0;
-    const int H4 = H & ~3;
-    for (int l = 1; l < L; ++l) {
-      for (int q = tid; q < H * H; q += NTHB) {
-        const int h = q / H, k = q - h * H;
-        wsc[h * 64 + k] = net.W[l][q] * act_d(net.act, act[l - 1][k]);
-      }
-      __syncthreads();  // wsc and Z_{l-1} complete
-      if (sw) {
-        float z[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) z[j][q] = 0.f;
-#ifndef DPI_BASE_SWEEP_UNROLL
-#define DPI_BASE_SWEEP_UNROLL 1
-#endif
-        constexpr int SWU = DPI_BASE_SWEEP_UNROLL;  // measurement knob: k-steps unrolled
-#pragma unroll SWU
-        for (int k = 0; k < H4; k += 4) {
-          const float4 z0 = *reinterpret_cast<const float4*>(&ztb[cz][k][4 * dg]);
-          const float4 z1 = *reinterpret_cast<const float4*>(&ztb[cz][k + 1][4 * dg]);
-          const float4 z2 = *reinterpret_cast<const float4*>(&ztb[cz][k + 2][4 * dg]);
-          const float4 z3 = *reinterpret_cast<const float4*>(&ztb[cz][k + 3][4 * dg]);
-          const float a0[4] = {z0.x, z0.y, z0.z, z0.w}, a1[4] = {z1.x, z1.y, z1.z, z1.w};
-          const float a2[4] = {z2.x, z2.y, z2.z, z2.w}, a3[4] = {z3.x, z3.y, z3.z, z3.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (j < RJ && hg + 16 * j < H) {
-              const float4 w = *reinterpret_cast<const float4*>(&wsc[(hg + 16 * j) * 64 + k]);
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                z[j][q] = fmaf(w.w, a3[q], fmaf(w.z, a2[q], fmaf(w.y, a1[q], fmaf(w.x, a0[q], z[j][q]))));
-            }
-        }
-        for (int k = H4; k < H; ++k) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (j < RJ && hg + 16 * j < H)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) z[j][q] = fmaf(wsc[(hg + 16 * j) * 64 + k], ztb[cz][k][4 * dg + q], z[j][q]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int h = hg + 16 * j;
-          if (j < RJ && h < H) {
-            *reinterpret_cast<float4*>(&ztb[cz ^ 1][h][4 * dg]) = make_float4(z[j][0], z[j][1], z[j][2], z[j][3]);
-            const float c = lamb[l][h] * act_d2(net.act, act[l][h]);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ud[q] = fmaf(c, z[j][q] * z[j][q], ud[q]);
-          }
-        }
-      }
-      cz ^= 1;
-      __syncthreads();  // before wsc is overwritten
-    }
-    if (sw)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) udp[hg][4 * dg + q] = ud[q];
-    __syncthreads();
-    if (tid < NXP_MAX) {
-      float a = 0.f;
-      for (int g = 0; g < 16; ++g) a += udp[g][tid];
-      hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
-    }
-    if (tid == 0) fb[i] = Cb;
-    return;
+    cz ^= 1;
+    __syncthreads();  // before wsc is overwritten
   }
-  const float u = block_sum_b(tid < H ? net.wout[tid] * act[L - 1][tid] : 0.f, red) + net.bout;
-  int cur = 0;
-  if (tid < H) dbuf[0][tid] = net.wout[tid] * act_d(net.act, act[L - 1][tid]);
+  if (sw)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) udp[hg][4 * dg + q] = ud[q];
   __syncthreads();
-  for (int l = L - 2; l >= 0; --l) {
-    // W_{l+1} (H_out, H_in) row-major is the transposed operand of this mat-vec
-    const float acc = matvec(net.W[l + 1], dbuf[cur], H);
-    if (tid < H) dbuf[cur ^ 1][tid] = acc * act_d(net.act, act[l][tid]);
-    cur ^= 1;
-    __syncthreads();
+  if (tid < NXP_MAX) {
+    float a = 0.f;
+    for (int g = 0; g < 16; ++g) a += udp[g][tid];
+    hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
   }
-  float gs = 0.f, gA = 0.f, gB = 0.f;
-  if (!Eq<KIND>::GRAD_FULL) {
-    gs = block_sum_b(tid < H ? net.c1[tid] * dbuf[cur][tid] : 0.f, red);
-  } else {
-    float A = 0.f, B = 0.f;
-    for (int d = tid; d < nx; d += NTHB) {
-      float z = 0.f;
-      for (int k = 0; k < H; ++k) z = fmaf(net.W1x[(size_t)k * nxp + d], dbuf[cur][k], z);
-      Eq<KIND>::gacc(e, d, xs[d], z, A, B);
-    }
-    gA = block_sum_b(A, red);
-    gB = block_sum_b(B, red);
-  }
-  if (tid == 0) fb[i] = Eq<KIND>::ffv(e, u, gs, gA, gB);  // state-dependent part
+  if (tid == 0) fb[i] = Cb;
 }
 
 struct PathArgs {
@@ -1559,6 +1680,68 @@ struct PathArgs {
   // k_noise_shared beside the previous batch's path launch, [n][nbp][2 (terminal, integral)][4 nb][P]
   const float* noise;
 };
+
+// The fused per-point baseline of k_paths_fb (dpi_sample_with_gradients as one launch: first-order
+// Cha / OU labels of MLP and zero nets, no TD), an argument of that kernel only: blocks
+// [0, nbase) run base_point for point blockIdx.x into rec and publish it on ready[i]; the path
+// blocks (blockIdx.x - nbase) draw their point themselves (smp: bitwise the base block's draws) and
+// wait for its record before they need it (base_poll, base_load).
+struct FusedBase {
+  int nbase;
+  float* rec;                 // [n][BREC]
+  unsigned long long* ready;  // [n]: (seq << 32) | ~seq once point i's record is out
+  uint32_t ready_seq;
+  SampleSpec smp;
+};
+
+// Fused baseline hand-off (MI355X_MICROARCH.md's producer / consumer forms): every storing wave
+// waits for its stores, a workgroup barrier, then one lane's agent-scope release and a relaxed
+// agent-scope store of the point's hand-off word.
+__device__ __forceinline__ unsigned long long ready_word(uint32_t seq) {
+  return ((unsigned long long)seq << 32) | (unsigned long long)(~seq);
+}
+__device__ __forceinline__ void base_publish(const FusedBase& fb, int i) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(fb.ready + i, ready_word(fb.ready_seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Consumer: one lane polls (relaxed agent-scope loads, s_sleep between) and runs one agent-scope
+// acquire (base_poll); a workgroup barrier the caller places after it; then every load of the record
+// (base_ok() says whether it came).  The poll is bounded (about half a second): a record that never
+// comes flags DPI_STATUS_HANDOFF and the point's labels NaN.
+constexpr int BASE_SPIN_MAX = 1 << 20;
+__device__ __forceinline__ int& base_ok() {
+  __shared__ int ok;
+  return ok;
+}
+__device__ __forceinline__ void base_poll(const FusedBase& fb, const PathArgs& a, int i) {
+  if (threadIdx.x == 0) {
+    const unsigned long long want = ready_word(fb.ready_seq);
+    int it = 0;
+    while (__hip_atomic_load(fb.ready + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want &&
+           ++it < BASE_SPIN_MAX)
+      __builtin_amdgcn_s_sleep(8);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const bool ok = it < BASE_SPIN_MAX;
+    base_ok() = ok;
+    if (!ok && a.rd_status) *(volatile int*)a.rd_status = DPI_STATUS_HANDOFF | DPI_STATUS_NONFINITE;
+  }
+}
+// A wave-uniform float into a scalar register (the builtin is int-typed: pass the bits)
+__device__ __forceinline__ float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+// A record value as a vector load (a uniform address would otherwise be a scalar-cache load, which
+// the acquire does not refresh)
+__device__ __forceinline__ float rec_load(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT));
+}
 
 // Noise sums of a (point, block, estimator part, wave slice) task: exactly the K-step loops of
 // k_paths' terminal / integral rollouts (same counters, same sequential sum per dimension, the same
@@ -1837,9 +2020,9 @@ __device__ __forceinline__ void hess_block(const EqDev& e, const NetDev& net, co
 // leaves as a perfect binary tree in block order — for nbp <= 64 exactly tree_sum's order, so the
 // moments and labels are bitwise k_reduce's — then finalizes (/M, + g(x), clip) and zeroes the
 // ticket for the next call (k_baseline zeroes it too).
-__device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, const float* out) {
+// rec != null (k_paths_fb): g(x) from the point's baseline record
+__device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, const float* rec) {
   __shared__ int last;
-  (void)out;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores complete
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1877,7 +2060,7 @@ __device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, co
     a.rd_moments[(size_t)i * 2 * F + c] = sum;
     if (a.rd_y && c < F) {
       float y = sum * a.rd_invM;
-      if (c == 0 && a.rd_add_g) y += a.gx[i];
+      if (c == 0 && a.rd_add_g) y += rec ? rec_load(rec + (size_t)i * BREC) : a.gx[i];
       a.rd_y[(size_t)i * F + c] = y != y ? y : fminf(fmaxf(y, -a.rd_bound), a.rd_bound);  // torch.clip
     }
   }
@@ -1892,15 +2075,33 @@ template <int KIND, int H, int L, bool SPLIT, bool TD>
 constexpr int k_paths_wgs() {
   return (KIND == DPI_EQ_GBM || TD || (KIND == DPI_EQ_OU && !SPLIT && H == 128 && L == 4)) ? 1 : 2;
 }
-template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
-__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k_paths(EqDev e, NetDev net, PathArgs a) {
+// The path launch body; FBT: the one-launch sample_with_gradients form (k_paths_fb), whose first
+// fb.nbase blocks are the points' base blocks — a kernel of its own, so the plain k_paths keeps its
+// register allocation (the hand-off's arguments live across the whole kernel).
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS, bool TD, int ACT, bool FBT>
+__device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, const PathArgs& a, const FusedBase& fb) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
   using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, Lds>;
   __shared__ SH sh;
-  const int i = blockIdx.x / a.nbp;
-  const int blk = blockIdx.x - i * a.nbp;
   constexpr bool GBM = KIND == DPI_EQ_GBM;
+  // fused baseline (k_paths_fb): the first fb.nbase blocks are the points' base blocks
+  constexpr bool FBC = FBT && !GBM && !HESS && !TD;
+  static_assert(FBC || !FBT, "the fused baseline: first-order Cha / OU labels, no TD");
+  constexpr bool FB = FBC;
+  if constexpr (FBC) {
+    static_assert(sizeof(BaseLds<NTH>) <= sizeof(SH), "base blocks overlay the path LDS");
+    if ((int)blockIdx.x < fb.nbase) {
+      base_point<KIND, ZERO, NTH>(e, net, a.tx, blockIdx.x, const_cast<float*>(a.gx), const_cast<float*>(a.fb),
+                                  const_cast<float*>(a.bx), fb.rec, fb.smp, a.tickets,
+                                  *reinterpret_cast<BaseLds<NTH>*>(&sh));
+      base_publish(fb, blockIdx.x);
+      return;
+    }
+  }
+  const unsigned bid = blockIdx.x - (FB ? (unsigned)fb.nbase : 0u);
+  const int i = bid / a.nbp;
+  const int blk = bid - i * a.nbp;
   // independent Philox chains per wave in the noise loops (2 vs 1: 2 % on the one- and two-wave-per-SIMD
   // kernels; 4 vs 2, round 3: 0.5 % first-order, 1.2 % GBM; round 4: GBM 8, Hessian labels 4)
   // (the u = 0 GBM instance keeps 4: at 8 its own allocation grew and the noise-floor launch ran
@@ -1916,7 +2117,9 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
   const int nxp = ZERO ? ((nx + 15) & ~15) : net.nxp;
   const bool TERM = a.flags & DPI_TERMINAL, INTG = a.flags & DPI_INTEGRAL;
   const float* txr = a.tx + (size_t)i * F;
-  const float t = txr[0];
+  // fused baseline: the block draws its point itself (the base block's draws, bitwise)
+  // (uniform: kept scalar, as the loaded t is)
+  const float t = FB ? uniform_f(sample_point_t(e, fb.smp, ig)) : txr[0];
   // horizon: T - t, or for TD t_next - t = dt where t_next = t + dt < T (data.py:539, :940)
   bool td_u = false;
   float tmt = e.T - t;
@@ -1924,12 +2127,26 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
     td_u = t + a.td_dt < e.T;
     if (td_u) tmt = a.td_dt;
   }
-  const float g_x = a.gx[i], f_b = a.fb[i];
+  float g_x = 0.f, f_b = 0.f;  // fused baseline: from the point's record (base_load)
+  if (!FB) {
+    g_x = a.gx[i];
+    f_b = a.fb[i];
+  }
   const float Kf = (float)a.K;
   // GBM prepared calls: phase 1's noise sums come from k_noise_shared (a wave-uniform branch)
   const bool PRE = GBM && !HESS && !TD && a.noise != nullptr;
 
-  for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
+  if (FB) {
+    if (tid < nb) {
+      float x[4];
+      sample_point_x4<KIND>(e, fb.smp, ig, tid, t, x);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sh.xsh[4 * tid + q] = 4 * tid + q < nx ? x[q] : 0.f;
+    }
+    for (int d = 4 * nb + tid; d < nxp; d += NTH) sh.xsh[d] = 0.f;
+  } else {
+    for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
+  }
   const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
   for (int idx = tid; idx < (nxpz - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
     const int d = 4 * nb + idx / P, p = idx % P;
@@ -1937,7 +2154,7 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
   }
   if (!ZERO) {
     for (int h = tid; h < H; h += NTH) {
-      sh.vec[h] = a.bx[(size_t)i * H + h];  // b1 + W1x x (from k_baseline)
+      if (!FB) sh.vec[h] = a.bx[(size_t)i * H + h];  // b1 + W1x x (from k_baseline; fused: base_load)
       sh.vec[H + h] = net.w1t[h];
       sh.vec[2 * H + h] = net.wout[h];
       sh.vec[3 * H + h] = net.c1[h];
@@ -2171,8 +2388,8 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
     tlast = true;  // measured faster, and the terminal sums are not live across the MLP (no spills)
   } else if constexpr (!GBM) {
     if (a.order == 1) tlast = (__builtin_amdgcn_s_getreg((3 << 11) | (16 << 6) | 4) & 1) != 0;  // HW_ID.TG_ID
-    else if (a.order == 2) tlast = (blockIdx.x & 1) != 0;
-    else if (a.order == 3) tlast = ((blockIdx.x >> 8) & 1) != 0;
+    else if (a.order == 2) tlast = (bid & 1) != 0;
+    else if (a.order == 3) tlast = ((bid >> 8) & 1) != 0;
     else if (a.order == 4) tlast = true;
   }
   // TD terminal value u(t_next, x + cT S_T) (data.py:941-942), per lane = path
@@ -2215,6 +2432,24 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
     // the integral rollout's writes into S are published by terminal_finish's barrier
     return uT;
   };
+  // fused baseline: the point's record, before the first use of g(x), f_b or bx.  base_poll runs on
+  // lane 0 ahead of a workgroup barrier (in the terminal-last order the one after the integral
+  // rollout, so the acquire overlaps the waves still rolling out); base_load after it.
+  auto base_poll_ = [&]() {
+    if constexpr (FBC) base_poll(fb, a, i);
+  };
+  auto base_load = [&]() {
+    if constexpr (FBC) {
+      const bool ok = base_ok() != 0;
+      const float* r = fb.rec + (size_t)i * BREC;
+      g_x = uniform_f(ok ? rec_load(r) : __builtin_nanf(""));  // uniform: scalar
+      f_b = uniform_f(ok ? rec_load(r + 1) : __builtin_nanf(""));
+      if (!ZERO) {
+        for (int h = tid; h < H; h += NTH) sh.vec[h] = r[32 + h];
+        __syncthreads();
+      }
+    }
+  };
   float ap;
   if constexpr (TD) {
     terminal_rollout();
@@ -2228,12 +2463,19 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
   } else if (!tlast) {
     terminal_rollout();
     integral_rollout();
+    if constexpr (FBC) {
+      base_poll_();
+      __syncthreads();
+      base_load();
+    }
     ap = terminal_finish();
     integrand();
     __syncthreads();
   } else {
     integral_rollout();
+    base_poll_();
     __syncthreads();
+    base_load();
     integrand();
     terminal_rollout();
     ap = terminal_finish();  // its barrier also publishes bsh
@@ -2302,8 +2544,19 @@ __global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k
   if constexpr (HESS) {
     hess_block<KIND, H, L, ZERO, SPLIT, ACT>(e, net, a, sh, i, blk, ig, m, s, smt, tmt, g_x, nxp);
   } else {
-    if (a.tickets) fused_reduce(a, i, F, out);
+    if (a.tickets) fused_reduce(a, i, F, FB ? fb.rec : nullptr);
   }
+}
+
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
+__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k_paths(EqDev e, NetDev net, PathArgs a) {
+  paths_body<KIND, H, L, ZERO, SPLIT, HESS, TD, ACT, false>(e, net, a, FusedBase{});
+}
+// The one-launch dpi_sample_with_gradients: fb.nbase base blocks ahead of the path blocks.
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, int ACT = DPI_ACT_ELU>
+__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, false>())) void k_paths_fb(EqDev e, NetDev net,
+                                                                                            PathArgs a, FusedBase fb) {
+  paths_body<KIND, H, L, ZERO, SPLIT, false, false, ACT, true>(e, net, a, fb);
 }
 
 }  // namespace dpi

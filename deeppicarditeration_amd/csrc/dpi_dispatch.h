@@ -42,6 +42,7 @@ struct Launch {
   bool td = false;    // k_paths with the TD estimators (problem td_dt > 0)
   SampleSpec smp{};   // baseline: sample the points in the same launch (smp.tx != null)
   int* tickets = nullptr;  // baseline: zero the fused reduce's per-point tickets
+  const FusedBase* fbase = nullptr;  // k_paths_fb: the one-launch sample_with_gradients (fused_base_ok)
 };
 
 // TDV: the TD-estimator k_paths variants, compiled in translation units of their own
@@ -49,9 +50,23 @@ struct Launch {
 // of the plain fused-MLP kernel (6 spills at 256 VGPRs instead of none at 252).
 // ACT: the hidden activation (DPI_ACT_*); the Tanh k_paths family lives in units of its own too
 // (dpi_paths_*_tanh.hip).  k_baseline is shape- and activation-generic (it reads net.act).
-template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU>
+// FBV: k_paths_fb, the one-launch sample_with_gradients (q.fbase), in translation units of its own
+// (dpi_paths_fb_*.hip: beside the plain kernels it perturbed their register allocation — the
+// OU 4 x 128 split instance went from 255 VGPRs to 256 and 3 spilled).  Instantiated where
+// fused_base_shape holds, which is where dpi_kernels.hip fused_base_ok selects it: Cha / OU with
+// ELU, zero nets and the fp16-split MLP instances (H % 32 == 0) — except OU 4 x 128, whose GMM
+// statistics beside the hand-off spill 3 VGPRs at two workgroups per CU (it keeps two launches).
+template <int KIND, int H, int L, bool Z, int ACT>
+constexpr bool fused_base_shape() {
+  return KIND != DPI_EQ_GBM && ACT == DPI_ACT_ELU && (Z || (H % 32 == 0 && !(KIND == DPI_EQ_OU && H == 128 && L == 4)));
+}
+template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU, bool FBV = false>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
-  if constexpr (TDV) {
+  if constexpr (FBV) {
+    if constexpr (fused_base_shape<KIND, H, L, Z, ACT>())
+      hipLaunchKernelGGL((k_paths_fb<KIND, H, L, Z, !Z, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a,
+                         *q.fbase);
+  } else if constexpr (TDV) {
     if constexpr (!Z && H % 32 == 0) {
       if (q.a->split)
         hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
@@ -63,10 +78,14 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
       hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
                          net->d, *q.a);
     }
-  } else if (q.baseline)
-    hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
-                       q.bx, q.hb, q.smp, q.tickets);
-  else if (q.hess) {
+  } else if (q.baseline) {
+    if constexpr (KIND == DPI_EQ_GBM)
+      hipLaunchKernelGGL((k_baseline_gbm<Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+                         q.bx, q.hb, q.smp, q.tickets);
+    else
+      hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+                         q.bx, q.smp, q.tickets);
+  } else if (q.hess) {
     if constexpr (KIND == DPI_EQ_GBM) {
       EqDev e2 = p->e;
       e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
@@ -92,18 +111,18 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
                        net->d, *q.a);
 }
 
-template <int KIND, bool TDV = false, int ACT = DPI_ACT_ELU>
+template <int KIND, bool TDV = false, int ACT = DPI_ACT_ELU, bool FBV = false>
 bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if constexpr (ACT == DPI_ACT_ELU) {  // zero nets and the (activation-generic) baseline: the ELU units
     if (net->d.kind == 0) {
-      do_launch<KIND, 16, 1, true, TDV>(p, net, q);
+      do_launch<KIND, 16, 1, true, TDV, DPI_ACT_ELU, FBV>(p, net, q);
       return true;
     }
   } else {
     if (net->d.kind == 0 || q.baseline) return false;
   }
   const int H = net->d.H, L = net->d.L;
-  if constexpr (!TDV && ACT == DPI_ACT_ELU) {
+  if constexpr (!TDV && !FBV && ACT == DPI_ACT_ELU) {
     if (q.baseline) {  // the baseline kernel is shape-generic
       if (KIND == DPI_EQ_GBM && H > 64) return false;
       do_launch<KIND, 16, 1, false, false>(p, net, q);
@@ -113,7 +132,7 @@ bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q)
   if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
 #define DPI_SHAPE(HH, LL)                      \
   if (H == HH && L == LL) {                    \
-    do_launch<KIND, HH, LL, false, TDV, ACT>(p, net, q); \
+    do_launch<KIND, HH, LL, false, TDV, ACT, FBV>(p, net, q); \
     return true;                               \
   }
     DPI_SHAPE(64, 3)
@@ -151,3 +170,5 @@ bool dispatch_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launc
 bool dispatch_td_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_td_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_td_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_fb_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_fb_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

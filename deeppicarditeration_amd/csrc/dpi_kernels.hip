@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -1168,9 +1169,10 @@ static int pis_chunk_wg() {
   return v;
 }
 
-// Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | [PIS rows] | partial[n][2F][nbp]  (256-B aligned)
+// Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | tickets[n] | rec[n][BREC] | ready[n] |
+// [PIS rows] | partial[n][nbp][slab_row] | ...  (256-B aligned)
 struct WsLayout {
-  size_t gx, fb, bx, hb, tk, rows, partial, rq, noise, nq, total;
+  size_t gx, fb, bx, hb, tk, rec, ready, rows, partial, rq, noise, nq, total;
   int rows_cap;
 };
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -1193,7 +1195,10 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F, bool noise = false) 
   w.bx = w.fb + al256((size_t)n * 4);
   w.hb = w.bx + al256((size_t)n * H * 4);
   w.tk = w.hb + al256((size_t)n * NXP_MAX * 4);  // the fused reduce's per-point tickets (k_paths)
-  w.rows = w.tk + al256((size_t)n * 4);
+  // the one-launch dpi_sample_with_gradients' per-point baseline records and hand-off words
+  w.rec = w.tk + al256((size_t)n * 4);
+  w.ready = w.rec + al256((size_t)n * BREC * 4);
+  w.rows = w.ready + al256((size_t)n * 8);
   w.rows_cap = 0;
   size_t rows_bytes = 0;
   if (net && net->d.kind == 2) {
@@ -1516,6 +1521,16 @@ extern "C" int dpi_sample_points_t(dpi_problem p, int n, uint64_t seed, uint32_t
 }
 
 static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if (q.fbase) {  // k_paths_fb (fused_base_ok)
+    switch (p->e.kind) {
+      case DPI_EQ_CHA:
+        return dispatch_fb_cha(p, net, q);
+      case DPI_EQ_OU:
+        return dispatch_fb_ou(p, net, q);
+      default:
+        return false;
+    }
+  }
   const bool td = q.td && !q.baseline && !q.hess;
   if (net->d.kind == 1 && net->d.act == DPI_ACT_TANH && !q.baseline) {  // the Tanh k_paths units
     switch (p->e.kind) {
@@ -1845,10 +1860,39 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   return 0;
 }
 
-// sample_with_gradients (picard/data.py:211-223) as one call: the points' draws 1-3 inside the
-// baseline launch (k_baseline with SampleSpec), then the fused rollout / label kernel whose last
-// block per point reduces and finalizes — two launches for first-order MLP / zero-net labels.
-// PISGradNet: dpi_sample_points_t + dpi_generate_with_gradients.
+// The one-launch dpi_sample_with_gradients (DPI_FUSED_BASE=0: two launches; read per call).
+static bool fused_base_on() {
+  const char* e = std::getenv("DPI_FUSED_BASE");
+  return !e || std::atoi(e) != 0;
+}
+// The nets and problems k_paths_fb is instantiated for (dpi_dispatch.h fused_base_shape):
+// first-order Cha / OU labels without TD, of zero nets or ELU MLP nets in the fp16-split mode
+// (H % 32 == 0, the fused-MLP instances; not OU 4 x 128); the rest runs the two-launch form.
+static bool fused_base_ok(dpi_problem p, dpi_net net) {
+  if (p->e.kind == DPI_EQ_GBM || p->td_dt > 0.f) return false;
+  if (net->d.kind == 0) return true;
+  const int H = net->d.H, L = net->d.L;
+  return net->d.kind == 1 && net->d.act == DPI_ACT_ELU && H % 32 == 0 && mlp_split(net) &&
+         !(p->e.kind == DPI_EQ_OU && H == 128 && L == 4);
+}
+// Hand-off sequence numbers: one per fused launch, process-wide, never 0, so a hand-off word left
+// in a workspace by an earlier launch (or never written) does not match this launch's.
+static std::atomic<uint32_t> g_ready_seq{0};
+static uint32_t next_ready_seq() {
+  uint32_t s;
+  do s = g_ready_seq.fetch_add(1, std::memory_order_relaxed) + 1u;
+  while (s == 0u);
+  return s;
+}
+
+// sample_with_gradients (picard/data.py:211-223) as one call.  First-order Cha / OU labels of MLP
+// and zero nets (no TD; <= 64 path blocks per point, so the label reduce runs in the path launch):
+// ONE k_paths launch of n base blocks (base_point: the point's draws 1-3, g(x), f_b, bx; published
+// per point) ahead of the n nbp path blocks, which draw their point themselves, roll out, and wait
+// for the point's record only before its first use — the baseline's latency-bound chain runs beside
+// the rollouts instead of ahead of them.  Otherwise the points' draws inside the baseline launch
+// (k_baseline with SampleSpec), then the rollout / label kernel.  PISGradNet:
+// dpi_sample_points_t + dpi_generate_with_gradients.
 int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, uint64_t seed, uint32_t epoch,
                               uint32_t point_base, float eps, int t_factors, int flags, float sample_bound, float* tx,
                               float* y, float* moments, void* ws, size_t ws_bytes, void* stream) {
@@ -1865,6 +1909,34 @@ int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, u
     if ((rc = dpi_sample_points_t(p, n, seed, epoch, point_base, eps, t_factors, tx, stream))) return rc;
     return dpi_generate_with_gradients(p, net, tx, n, M, K, seed, epoch, point_base, flags, sample_bound, y, moments, ws,
                                        ws_bytes, stream);
+  }
+  if (fused_base_ok(p, net) && M % P == 0 && M / P <= 64 && fused_reduce_on() && fused_base_on()) {
+    WsLayout wl;
+    PathArgs a;
+    if ((rc = label_args(p, net, tx, n, M, K, seed, epoch, point_base, 0, M, flags, true, moments, ws, ws_bytes, &wl,
+                         &a)))
+      return rc;
+    char* b = (char*)ws;
+    a.tickets = (int*)(b + wl.tk);
+    a.rd_moments = moments;
+    a.rd_y = y;
+    a.rd_status = net_status(net);
+    a.rd_invM = 1.0f / (float)M;
+    a.rd_bound = sample_bound;
+    a.rd_add_g = (flags & DPI_TERMINAL) ? 1 : 0;
+    FusedBase fb{};
+    fb.nbase = n;
+    fb.rec = (float*)(b + wl.rec);
+    fb.ready = (unsigned long long*)(b + wl.ready);
+    fb.ready_seq = next_ready_seq();
+    fb.smp = sample_spec(p, seed, epoch, point_base, eps, t_factors, tx);
+    Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n + n * a.nbp, (hipStream_t)stream};
+    q.fbase = &fb;
+    if (!dispatch_any(p, net, q))
+      return fail(DPI_ERR_UNSUPPORTED, "sample_with_gradients: unsupported equation/network shape");
+    HIPCHK(hipGetLastError());
+    base_tag_set(ws, n);  // the base blocks zeroed the tickets and left the baseline in ws
+    return 0;
   }
   if ((rc = dpi_sample_points_baseline(p, net, n, seed, epoch, point_base, eps, t_factors, tx, ws, ws_bytes, stream)))
     return rc;

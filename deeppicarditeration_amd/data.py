@@ -52,6 +52,14 @@ IMMEDIATE_SLOT = 0
 UNCHECKED_SLOT = _lib.DPI_STATUS_SLOTS - 1
 
 
+def _check_handoff(flag):
+    """DPI_STATUS_HANDOFF: a one-launch sample_with_gradients path block never saw its point's
+    baseline (an internal failure, not a range problem): no fp32 repair, an error."""
+    if flag & _lib.DPI_STATUS_HANDOFF:
+        raise _lib.DPIError("fused baseline hand-off timed out in dpi_sample_with_gradients (DPI_FUSED_BASE=0 "
+                            "runs the two-launch form)")
+
+
 class RangeGroup:
     """The range guard of a group of label calls, checked once for the whole group instead of with
     a stream synchronisation per call (include/dpi.h dpi_net_status_slot / _peek).
@@ -124,6 +132,7 @@ class RangeGroup:
             flag = self.reduce_flag(flag)
         self.done = True
         self.gen._release_slot(self.slot)
+        _check_handoff(flag)
         if flag & _lib.DPI_STATUS_NONFINITE:
             self.gen._repair(self.calls, self.reduce_flag)
         self.calls = []
@@ -419,8 +428,9 @@ class OnlineDataGenerator:
 
     def sample_with_gradients(self, n_batch):
         """data.py:211-223: (tx, clip(u_ux)) with u_ux (n, 1+nx).  One C-ABI call where it fits
-        (dpi_sample_with_gradients: the sampling inside the baseline launch, the label reduce
-        inside the path launch); tx and labels are bitwise those of the separate calls."""
+        (dpi_sample_with_gradients: for first-order Cha / OU labels one launch, the per-point
+        baseline beside the rollouts and the label reduce in the path launch); tx and labels are
+        bitwise those of the separate calls."""
         MT, MI = self.n_estimate_terminal, self.n_estimate_integral
         if MT == MI and MT <= PATHS_PER_CALL_MAX:
             pb = self._take_points(n_batch)
@@ -430,17 +440,28 @@ class OnlineDataGenerator:
 
     def sample_generate(self, n_batch, point_base, bound=None, on_moments_begin=None, on_moments_end=None):
         """Points at counters [point_base, point_base + n) and their clipped labels (no range guard):
-        (tx, y) from two launches — dpi_sample_points_baseline (the sampling inside the baseline
-        launch), then dpi_label_moments_finalize (the label reduce inside the path launch);
-        last_moments as _generate.  on_moments_*: called around the second (bench timing)."""
+        (tx, y) from dpi_sample_with_gradients — for first-order Cha / OU labels one launch (n
+        baseline workgroups ahead of the path workgroups, the label reduce in each point's last path
+        workgroup), otherwise the sampling inside the baseline launch, then the path launch;
+        last_moments as _generate.  on_moments_*: called around the call (bench timing)."""
+        n, F = n_batch, 1 + self.equation.nx
         M = self.n_estimate_integral
-        ws = self._workspace(n_batch, M)
-        tx = self.sample_points_baseline(n_batch, point_base, ws)
+        ws = self._workspace(n, M)
+        tx = torch.empty(n, F, dtype=torch.float32, device=self._device)
+        y = torch.empty(n, F, dtype=torch.float32, device=self._device)
+        mom = torch.empty(n, 2, F, dtype=torch.float32, device=self._device)
+        b = self.sample_bound if bound is None else bound
+        self._configure_problem()
         if on_moments_begin:
             on_moments_begin()
-        y, self.last_moments = self.label_moments_finalize(tx, point_base, M, _lib.DPI_BOTH, ws, bound)
+        _lib.check(self.lib.dpi_sample_with_gradients(self.problem, self.net.handle, n, M, self.K, self.seed,
+                                                      self.epoch, point_base, self.eps, self.t_factors,
+                                                      _lib.DPI_BOTH, b, _ptr(tx), _ptr(y), _ptr(mom), _ptr(ws),
+                                                      ws.numel(), _stream(self._device)),
+                   "dpi_sample_with_gradients")
         if on_moments_end:
             on_moments_end()
+        self.last_moments = mom
         return tx, y
 
     def sample_points_baseline(self, n_batch, point_base, ws, out=None):
@@ -712,6 +733,7 @@ class OnlineDataGenerator:
             self._select_slot(prev)
         if reduce_flag is not None:
             flag = reduce_flag(flag)
+        _check_handoff(flag)
         if not flag & _lib.DPI_STATUS_NONFINITE:
             return y
         if self._fp32_fallback:

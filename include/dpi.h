@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 4
+#define DPI_ABI_VERSION 5
 
 /* error codes */
 #define DPI_OK 0
@@ -167,8 +167,12 @@ int dpi_net_set_precision(dpi_net net, int mode);
  * dpi_net_status: the selected slot after the work queued on `stream` (a synchronisation) and,
  * with clear != 0, resets it.  dpi_net_status_slot: select `slot` for the calls enqueued from now
  * on and, with clear != 0, zero it first (a host store: no enqueued call may still flag into it).
- * Zero networks have no status words: their reads return 0.  Replaces no reference interface. */
+ * Zero networks have no status words: their reads return 0.  Replaces no reference interface.
+ * DPI_STATUS_HANDOFF (stored together with DPI_STATUS_NONFINITE, the point's labels NaN): a path
+ * block of the one-launch dpi_sample_with_gradients did not see its point's baseline within its
+ * bounded wait — an internal failure, never a range problem. */
 #define DPI_STATUS_NONFINITE 1
+#define DPI_STATUS_HANDOFF 2
 #define DPI_STATUS_SLOTS 64
 int dpi_net_status(dpi_net net, int clear, void* stream, int* status);
 int dpi_net_status_slot(dpi_net net, int slot, int clear);
@@ -256,8 +260,12 @@ int dpi_generate_with_gradients(dpi_problem p, dpi_net net, const float* tx, int
 
 /* sample_with_gradients(n): the n points of dpi_sample_points_t (eps, t_factors, point_base as
  * there) into tx (n, 1+nx), then dpi_generate_with_gradients on them — tx, y and moments bitwise
- * those of the two separate calls.  MLP and zero networks run it as two launches (the sampling
- * inside the baseline launch, the label reduce inside the path launch). */
+ * those of the two separate calls, and the workspace's baseline that of dpi_point_baseline.
+ * First-order Cha / OU labels of MLP and zero networks (no TD, M <= 4096) run as ONE launch: n
+ * baseline workgroups ahead of the path workgroups, which draw their point themselves and wait for
+ * its baseline (an in-launch hand-off) before the network evaluation; the label reduce runs in the
+ * path launch (DPI_FUSED_BASE=0: two launches, the sampling inside the baseline launch).  GBM: two
+ * launches; PISGradNet: dpi_sample_points_t + dpi_generate_with_gradients. */
 int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, uint64_t seed, uint32_t epoch,
                               uint32_t point_base, float eps, int t_factors, int flags, float sample_bound,
                               float* tx, float* y, float* moments, void* ws, size_t ws_bytes, void* stream);

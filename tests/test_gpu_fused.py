@@ -1,7 +1,9 @@
-"""The two-launch sample_with_gradients (round 4): the points sampled inside the baseline launch
-(dpi_sample_points_baseline) and the label reduce inside the path launch (k_paths' last block per
-point, DPI_FUSED_REDUCE) against the separate launches they replace — k_sample_points,
-k_baseline, k_paths, k_reduce — bit for bit (reference picard/data.py:211-223)."""
+"""sample_with_gradients in fewer launches against the separate launches they replace —
+k_sample_points, k_baseline, k_paths, k_reduce — bit for bit (reference picard/data.py:211-223):
+the one-launch form (round 6, k_paths_fb: base workgroups ahead of the path workgroups, an in-launch
+hand-off per point) and the two-launch form (round 4, DPI_FUSED_BASE=0: the points sampled inside
+the baseline launch, dpi_sample_points_baseline), both with the label reduce inside the path launch
+(k_paths' last block per point, DPI_FUSED_REDUCE)."""
 import pytest
 import torch
 
@@ -42,11 +44,15 @@ def _separate(gen, n, pb):
 @pytest.mark.parametrize("kind,n,M,K,t_uniform", [("cha", 16, 4096, 50, True), ("cha", 5, 192, 3, False),
                                                   ("gbm", 8, 1024, 4, True), ("ou", 3, 128, 4, True),
                                                   ("zero", 4, 64, 2, True)])
-def test_two_launch_sample_with_gradients_is_bitwise_the_separate_launches(kind, n, M, K, t_uniform, monkeypatch):
+@pytest.mark.parametrize("fused_base", ["1", "0"])
+def test_two_launch_sample_with_gradients_is_bitwise_the_separate_launches(kind, n, M, K, t_uniform, fused_base,
+                                                                           monkeypatch):
+    """fused_base "1": one launch for Cha / OU / zero nets (GBM keeps two); "0": two launches."""
     gen = _make(kind, M, K, t_uniform)
     monkeypatch.setenv("DPI_FUSED_REDUCE", "0")
     tx0, y0, mom0 = _separate(gen, n, 40)
     monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    monkeypatch.setenv("DPI_FUSED_BASE", fused_base)
     tx1, y1 = gen.sample_generate(n, 40)
     mom1 = gen.last_moments
     torch.cuda.synchronize()
@@ -54,6 +60,59 @@ def test_two_launch_sample_with_gradients_is_bitwise_the_separate_launches(kind,
     assert torch.equal(mom0, mom1)
     assert torch.equal(y0, y1)
     assert torch.isfinite(y1).all()
+
+
+@pytest.mark.parametrize("n,M", [(512, 128), (64, 4096), (1, 64), (300, 1024)])
+def test_one_launch_many_points(n, M, monkeypatch):
+    """k_paths_fb with many hand-offs: more base workgroups than one round of the grid holds (512
+    points), a point per 64 path workgroups (64 x 4096), one point, a ragged count."""
+    gen = _make("cha", M, 3)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "0")
+    tx0, y0, mom0 = _separate(gen, n, 11)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    tx1, y1 = gen.sample_generate(n, 11)
+    torch.cuda.synchronize()
+    assert torch.equal(tx0, tx1)
+    assert torch.equal(mom0, gen.last_moments)
+    assert torch.equal(y0, y1)
+
+
+def test_one_launch_repeated_on_one_workspace_and_leaves_the_baseline(monkeypatch):
+    """Three one-launch calls on one workspace (each its own hand-off sequence number, so the words
+    the previous call left never match) give the same points and labels; afterwards the workspace
+    holds the baseline dpi_point_baseline leaves, so a label call on it matches too."""
+    gen = _make("cha", 1024, 3)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    outs = [gen.sample_generate(6, 5) for _ in range(3)]
+    for tx, y in outs[1:]:
+        assert torch.equal(tx, outs[0][0]) and torch.equal(y, outs[0][1])
+    ws = gen._workspace(6, 1024)
+    y2, _ = gen.label_moments_finalize(outs[0][0], 5, 1024, L.DPI_BOTH, ws)
+    assert torch.equal(y2, outs[0][1])
+
+
+@pytest.mark.parametrize("variant", ["fp32", "tanh", "td", "ou128x4", "h16"])
+def test_nets_without_the_one_launch_form_keep_two_launches(variant, monkeypatch):
+    """Exact-fp32 mode, Tanh nets, the TD estimators, OU with a 4 x 128 net and 16-wide nets have no
+    k_paths_fb instance: the call runs two launches and still equals the separate launches."""
+    torch.manual_seed(0)
+    eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
+    if variant == "ou128x4":
+        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+                                   alpha_scale=4.0)
+    act = "Tanh" if variant == "tanh" else "ELU"
+    widths = [128] * 4 if variant == "ou128x4" else [16, 16] if variant == "h16" else [64, 64]
+    net = dpi.construct_mlp(1 + NX, 1, widths, [act] * len(widths), None)
+    gen = dpi.OnlineDataGenerator(eq, net, 10, 3, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                  n_estimate_integral=256, n_euler_steps=3, seed=7,
+                                  estimate_delta_t=0.25 if variant == "td" else None)
+    if variant == "fp32":
+        gen.use_fp32()
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "0")
+    tx0, y0, mom0 = _separate(gen, 5, 2)
+    monkeypatch.setenv("DPI_FUSED_REDUCE", "1")
+    tx1, y1 = gen.sample_generate(5, 2)
+    assert torch.equal(tx0, tx1) and torch.equal(y0, y1) and torch.equal(mom0, gen.last_moments)
 
 
 def test_fused_reduce_repeated_calls_reuse_the_tickets(monkeypatch):

@@ -34,7 +34,7 @@ def kernels():
 def test_every_kernel_is_found(kernels):
     names = [k["name"] for k in kernels]
     for fam in ("dpi::k_pis_net<", "dpi::k_pis_rollout<", "dpi::k_gemm_x3h<", "dpi::k_gemm_x3<", "dpi::k_paths<",
-                "dpi::k_reduce", "dpi::k_baseline<"):
+                "dpi::k_paths_fb<", "dpi::k_reduce", "dpi::k_baseline<", "dpi::k_baseline_gbm<"):
         assert any(fam in n for n in names), fam
 
 

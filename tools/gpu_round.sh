@@ -2,7 +2,7 @@
 # One GPU call of a round, by stages: GPU tests, bench lines for every workload, kernel traces (one
 # stream for HJB), the counter list, the VALU / HBM PMC passes, same-box A/B against the round-5
 # package (ab, probe: tools/variants/r05pkg), the N = 2 gloo rehearsals and the RCCL smoke.
-# usage: tools/gpu_round.sh <tag> [tests|bench|trace|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
+# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
 #        outputs under gpurun_out/<tag>/
 set -e
 tag=${1:-r02}; shift || true
@@ -28,6 +28,12 @@ for w in $what; do
     done
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
       python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline --no-prepare > $out/trace_hjb_onestream.log 2>&1 ;;
+  traceb)  # the Burgers bench line's kernels only, one-launch and two-launch sample_with_gradients
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_burgers -o trace --output-format csv -- \
+      python bench.py --workload burgers --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_burgers.log 2>&1
+    DPI_FUSED_BASE=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_burgers_fb0 -o trace \
+      --output-format csv -- python bench.py --workload burgers --steps 10 --warmup 2 --no-cpu-baseline \
+      > $out/trace_burgers_fb0.log 2>&1 ;;
   hjb)
     run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
@@ -35,6 +41,14 @@ for w in $what; do
   hjbprep)
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_prepare -o trace --output-format csv -- \
       python bench.py --workload hjb --steps 10 --warmup 2 --no-cpu-baseline > $out/trace_hjb_prepare.log 2>&1 ;;
+  fused)
+    run 900 $out/gpu_fused.log python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_canary.py -v --timeout 300 \
+      --timeout-method thread ;;
+  fbab)  # Burgers: the one-launch sample_with_gradients against the two-launch form, interleaved
+    for r in 1 2; do
+      DPI_FUSED_BASE=1 run 300 $out/bench_burgers_fb1_$r.log python bench.py
+      DPI_FUSED_BASE=0 run 300 $out/bench_burgers_fb0_$r.log python bench.py
+    done ;;
   ab)
     tools/ab_bench.sh $tag/ab burgers hjb gbm gbm_hess ;;
   probe)
