@@ -23,6 +23,7 @@ ShardedLabeler's two-phase begin/end with its asynchronous all_gather_into_tenso
 all-reduce — is the code the RCCL run executes.
 """
 import argparse
+import ctypes
 import json
 import os
 import re
@@ -282,8 +283,22 @@ def main():
     labeler = ShardedLabeler(gen, rank=rank, world=world, group=None if dist is None else dist.group.WORLD,
                              sample_ahead=bool(wl.get("pis")) and os.environ.get("DPI_BENCH_SAMPLE_AHEAD", "1") == "1")
 
-    # path-kernel timing with events on the stream the kernels run on (torch's current stream)
+    # path-kernel timing: the library's launch timers (dpi_launch_timer_arm) put HIP start / stop
+    # events on the timed launch's own dispatch packet (hipExtLaunchKernel) — k_paths / k_paths_fb,
+    # or k_pis_net for PISGradNet — so kernel_ms is that launch's duration, not a window of the
+    # stream that holds a cross-stream wait or the marker packets of torch events
     ev = []
+    tlib = L.load()
+
+    def arm_timer():
+        slot = len(ev) % L.DPI_LAUNCH_TIMERS
+        L.check(tlib.dpi_launch_timer_arm(slot), "dpi_launch_timer_arm")
+        ev.append(slot)
+
+    def timer_ms(slot):
+        ms = ctypes.c_float()
+        L.check(tlib.dpi_launch_timer_ms(slot, ctypes.byref(ms)), "dpi_launch_timer_ms")
+        return ms.value
 
     # N > 1: two-phase labels, so step i's RCCL all-gather (on RCCL's stream) overlaps step i+1's
     # kernels; every step's full work (sampling, moments, gather, reduce, finalize) still runs
@@ -302,33 +317,25 @@ def main():
             capture.update(tx=tx_, pb=pb_, y=y)
         return y
 
-    # Launch-time events go on every EV_EVERY-th step only: a timing event between two dependent
-    # launches makes the command processor drain and stamp (≈5 µs each, two per step — 2.7 % of a
-    # Burgers step), so instrumenting every step would slow the timed region it measures.
+    # The timed launch of every EV_EVERY-th step (timer events on a dispatch packet are cheap, but
+    # the stop event's completion signal still makes the launch's end visible to the host)
     EV_EVERY = 4
     nstep = [0]
 
     def step():
         sampled = nstep[0] % EV_EVERY == 0
         nstep[0] += 1
-        if sampled:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            rec0, rec1 = (lambda: e0.record()), (lambda: e1.record())
-        else:
-            rec0 = rec1 = None
+        rec0 = arm_timer if sampled else None
+        rec1 = None
         if args.prepare and pipelined:  # next batch's sampling + baseline on a low-priority side stream
             prep = labeler.prepare(N_POINTS)
             begun.append(prep[:2])
             pending.append(labeler.begin(prepared=prep, on_moments_begin=rec0, on_moments_end=rec1))
-            if sampled:
-                ev.append((e0, e1))
             return finish(pending.pop(0)) if len(pending) > 1 else None
-        if not wl.get("hess") and not pipelined:  # one rank: sampling inside the baseline launch (2 launches)
+        if not wl.get("hess") and not pipelined:  # one rank: sampling inside the path launch (one launch)
             tx, pb, y = labeler.sample_labels(N_POINTS, on_moments_begin=rec0, on_moments_end=rec1)
             begun.append((tx, pb))
             pending.append(("done", y))
-            if sampled:
-                ev.append((e0, e1))
             return finish(pending.pop(0))
         tx, pb = gen.sample_t_and_x(N_POINTS)
         begun.append((tx, pb))
@@ -341,8 +348,6 @@ def main():
         else:
             pending.append(("done", labeler.labels(tx, pb, on_moments_begin=rec0, on_moments_end=rec1)))
             y = finish(pending.pop(0))
-        if sampled:
-            ev.append((e0, e1))
         return y
 
     # RangeGroups of the steps not yet verified ("step": one per step, verified one step behind;
@@ -414,7 +419,7 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
-    k_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    k_ms = sum(timer_ms(slot) for slot in ev) / len(ev)
     if dist:
         t = torch.tensor([dt, k_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -464,13 +469,12 @@ def main():
         ws0 = gen0.point_baseline(tx0)
         fl = []
         for it in range(8):
-            f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            f0.record()
+            slot = it % L.DPI_LAUNCH_TIMERS
+            L.check(tlib.dpi_launch_timer_arm(slot), "dpi_launch_timer_arm")
             gen0.label_moments(tx0, pb0, M_PER_GPU, 0, M_PER_GPU, L.DPI_BOTH, ws0)
-            f1.record()
-            fl.append((f0, f1))
+            fl.append(slot)
         torch.cuda.synchronize()
-        floor_ms = sum(a.elapsed_time(b) for a, b in fl[2:]) / len(fl[2:])
+        floor_ms = sum(timer_ms(slot) for slot in fl[2:]) / len(fl[2:])
     path_labels_per_step = N_POINTS * M  # all ranks together
     value = path_labels_per_step * args.steps / dt
     if rank == 0:

@@ -2,6 +2,8 @@
 // dispatch; dispatch<KIND> is instantiated once per equation kind in dpi_paths_{cha,ou,gbm}.hip
 // so the three families compile in parallel.
 #pragma once
+#include <hip/hip_ext.h>
+
 #include "dpi_device.h"
 
 using namespace dpi;
@@ -43,7 +45,13 @@ struct Launch {
   SampleSpec smp{};   // baseline: sample the points in the same launch (smp.tx != null)
   int* tickets = nullptr;  // baseline: zero the fused reduce's per-point tickets
   const FusedBase* fbase = nullptr;  // k_paths_fb: the one-launch sample_with_gradients (fused_base_ok)
+  // dpi_launch_timer_arm: the path launch's own start / stop timestamps (hipExtLaunchKernel records
+  // them on the dispatch packet itself — no marker packets between the launches); null: untimed
+  hipEvent_t t0 = nullptr, t1 = nullptr;
 };
+// The path launches (k_paths, k_paths_fb) of a Launch, with its timer events when armed.
+#define DPI_PATH_LAUNCH(KERN, q, ...) \
+  hipExtLaunchKernelGGL(KERN, dim3((q).nblocks), dim3(NTH), 0, (q).st, (q).t0, (q).t1, 0, __VA_ARGS__)
 
 // TDV: the TD-estimator k_paths variants, compiled in translation units of their own
 // (dpi_paths_td_*.hip): sharing a unit with the plain kernels perturbs the register allocation
@@ -64,18 +72,17 @@ template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU, bool 
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if constexpr (FBV) {
     if constexpr (fused_base_shape<KIND, H, L, Z, ACT>())
-      hipLaunchKernelGGL((k_paths_fb<KIND, H, L, Z, !Z, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e, net->d, *q.a,
+      DPI_PATH_LAUNCH((k_paths_fb<KIND, H, L, Z, !Z, ACT>), q, p->e, net->d, *q.a,
                          *q.fbase);
   } else if constexpr (TDV) {
     if constexpr (!Z && H % 32 == 0) {
       if (q.a->split)
-        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+        DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, true, false, true, ACT>), q, p->e,
                            net->d, *q.a);
       else
-        hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
-                           p->e, net->d, *q.a);
+        DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, false, true, ACT>), q, p->e, net->d, *q.a);
     } else {
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, true, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+      DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, false, true, ACT>), q, p->e,
                          net->d, *q.a);
     }
   } else if (q.baseline) {
@@ -91,23 +98,21 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
       e2.sdgd_v = 0;  // the Hessian estimators evaluate f with the full Hessian (data.py:856, :1262-1272)
       if constexpr (!Z && H % 32 == 0) {
         if (q.a->split) {
-          hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, true, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
-                             e2, net->d, *q.a);
+          DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, true, true, false, ACT>), q, e2, net->d, *q.a);
           return;
         }
       }
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, true, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, e2,
+      DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, true, false, ACT>), q, e2,
                          net->d, *q.a);
     }
   } else if constexpr (!Z && H % 32 == 0) {
     if (q.a->split)
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, true, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+      DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, true, false, false, ACT>), q, p->e,
                          net->d, *q.a);
     else
-      hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st,
-                         p->e, net->d, *q.a);
+      DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, false, false, ACT>), q, p->e, net->d, *q.a);
   } else
-    hipLaunchKernelGGL((k_paths<KIND, H, L, Z, false, false, false, ACT>), dim3(q.nblocks), dim3(NTH), 0, q.st, p->e,
+    DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, false, false, ACT>), q, p->e,
                        net->d, *q.a);
 }
 

@@ -481,6 +481,50 @@ extern "C" {
 
 int dpi_abi_version(void) { return DPI_ABI_VERSION; }
 
+// ---- launch timers (dpi_launch_timer_*): start / stop events recorded on the timed path
+// launch's own dispatch packet
+struct LaunchTimer {
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  bool recorded = false;
+};
+static LaunchTimer g_timers[DPI_LAUNCH_TIMERS];
+static std::mutex g_timer_mu;
+static thread_local int g_timer_armed = -1;
+
+int dpi_launch_timer_arm(int slot) {
+  if (slot < 0 || slot >= DPI_LAUNCH_TIMERS) return fail(DPI_ERR_ARG, "launch_timer_arm: slot out of range");
+  std::lock_guard<std::mutex> lk(g_timer_mu);
+  LaunchTimer& t = g_timers[slot];
+  if (!t.t0) {
+    HIPCHK(hipEventCreate(&t.t0));
+    HIPCHK(hipEventCreate(&t.t1));
+  }
+  t.recorded = false;
+  g_timer_armed = slot;
+  return 0;
+}
+
+int dpi_launch_timer_ms(int slot, float* ms) {
+  if (slot < 0 || slot >= DPI_LAUNCH_TIMERS || !ms) return fail(DPI_ERR_ARG, "launch_timer_ms: bad arguments");
+  LaunchTimer& t = g_timers[slot];
+  if (!t.recorded) return fail(DPI_ERR_ARG, "launch_timer_ms: no launch recorded on this slot since it was armed");
+  HIPCHK(hipEventSynchronize(t.t1));
+  HIPCHK(hipEventElapsedTime(ms, t.t0, t.t1));
+  return 0;
+}
+
+// The armed timer's events for the path launch about to be enqueued (and disarm), or nulls.
+static void take_timer(hipEvent_t& t0, hipEvent_t& t1) {
+  t0 = t1 = nullptr;
+  if (g_timer_armed < 0) return;
+  LaunchTimer& t = g_timers[g_timer_armed];
+  g_timer_armed = -1;
+  t0 = t.t0;
+  t1 = t.t1;
+  t.recorded = true;
+}
+
+
 int dpi_last_error(char* buf, size_t len) {
   if (buf && len) {
     std::strncpy(buf, g_err.c_str(), len - 1);
@@ -1369,8 +1413,11 @@ static PisRows pis_chain_x3(const NetPisDev& pd, float* rows, int R, hipStream_t
     // DPI_PIS_NT: 2 (default) non-temporal row loads, plain stores; 1 both non-temporal; 0 neither
     const char* e = std::getenv("DPI_PIS_NT");
     const int ntm = e ? (std::atoi(e) == 1 ? 3 : std::atoi(e) == 0 ? 0 : 1) : 1;
+    hipEvent_t t0, t1;
+    take_timer(t0, t1);
     auto launch = [&](auto ntc, auto nlc) {
-      hipLaunchKernelGGL((k_pis_net<decltype(ntc)::value, decltype(nlc)::value>), grid, block, 0, st, pd, rows, L, R);
+      hipExtLaunchKernelGGL((k_pis_net<decltype(ntc)::value, decltype(nlc)::value>), grid, block, 0, st, t0, t1, 0, pd,
+                            rows, L, R);
     };
     auto by_depth = [&](auto ntc) {
       switch (pd.L) {
@@ -1832,6 +1879,7 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
+    take_timer(q.t0, q.t1);
     if ((flags & DPI_PREPARED) && stages_prepare(p, net)) a.noise = (const float*)(b + w.noise);
     if (nbp <= 64 && fused_reduce_on()) {  // k_paths' last block per point reduces and finalizes
       if (!base_tag_ok(ws, n))
@@ -1932,6 +1980,7 @@ int dpi_sample_with_gradients(dpi_problem p, dpi_net net, int n, int M, int K, u
     fb.smp = sample_spec(p, seed, epoch, point_base, eps, t_factors, tx);
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n + n * a.nbp, (hipStream_t)stream};
     q.fbase = &fb;
+    take_timer(q.t0, q.t1);
     if (!dispatch_any(p, net, q))
       return fail(DPI_ERR_UNSUPPORTED, "sample_with_gradients: unsupported equation/network shape");
     HIPCHK(hipGetLastError());
@@ -2196,6 +2245,7 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   hipStream_t st = (hipStream_t)stream;
   Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
   q.hess = true;
+  take_timer(q.t0, q.t1);
   if (!dispatch_any(p, net, q))
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: unsupported network shape (GBM: width <= 64)");
   HIPCHK(hipGetLastError());

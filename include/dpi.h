@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 5
+#define DPI_ABI_VERSION 6
 
 /* error codes */
 #define DPI_OK 0
@@ -182,6 +182,16 @@ int dpi_net_status_peek(dpi_net net, int slot, int* status);
  * (deeppicarditeration_amd/build.py source_hash), NUL-terminated into buf; returns its length.
  * The host layer refuses a library whose identity differs from the tree's sources. */
 int dpi_build_id(char* buf, size_t len);
+
+/* Measurement (bench.py's kernel time; no reference counterpart).  dpi_launch_timer_arm(slot)
+ * arms timer slot (0 <= slot < DPI_LAUNCH_TIMERS) for the calling thread: the next path launch it
+ * enqueues (k_paths / k_paths_fb of a label call, or k_pis_net of a PISGradNet label call) records
+ * the slot's start / stop events on its own dispatch packet (hipExtLaunchKernel), and disarms it.
+ * dpi_launch_timer_ms waits for the slot's stop event and writes the launch's duration in ms;
+ * DPI_ERR_ARG if the slot never recorded a launch since it was last armed. */
+#define DPI_LAUNCH_TIMERS 256
+int dpi_launch_timer_arm(int slot);
+int dpi_launch_timer_ms(int slot, float* ms);
 
 /* Device workspace a dpi_* call on (p, net, n points, M paths) needs. */
 size_t dpi_workspace_bytes(dpi_problem p, dpi_net net, int n, int M);
