@@ -70,6 +70,12 @@ WORKLOADS = {
                      desc="Fully-nonlinear case_1 100d (GBM), generate_with_gradients_and_hessians: labels "
                           "(u, u_x, u_xx) = 1 + 100 + 10,000 wide, full-Hessian f at 3 points per path, 64 points x "
                           "1024 MC paths per GPU, K=50, MLP 101-64x3-1 ELU"),
+    # not a BASELINE config: the state dimension above 128 (the wide first-order instances)
+    "burgers_nx256": dict(cfg="configs[1] shape at nx = 256 (not a BASELINE config)", eq="Cha", nx=256,
+                          widths=[128] * 4, points=16, m_per_gpu=4096, K=50, sdgd=0, flop=3.52e5, peak="split",
+                          kernel="k_paths<Cha,128,4,split,nx<=256> (one workgroup per CU) after k_baseline",
+                          desc="Burgers 256d T=1 (Cha k=5), 16 points x 4096 MC paths per GPU, K=50 EM steps, "
+                               "MLP 257-128x4-1 ELU"),
     "gbm": dict(cfg="configs[4]", eq="GBMEquationComplexExact", widths=[64] * 3, points=64, m_per_gpu=1024, K=50,
                 sdgd=100, flop=1.68e6, survey_flop=3.36e6, peak="split",
                 kernel="k_paths<GBM,64,3> + k_reduce per dpi_label_moments call",
@@ -105,30 +111,32 @@ def parse():
 
 
 def _make(wl, dpi):
+    nx = wl.get("nx", NX)
     torch.manual_seed(0)
     if wl["eq"] == "Cha":
-        eq = dpi.Cha(NX, 1.0, 5.0, 1.0)
+        eq = dpi.Cha(nx, 1.0, 5.0, 1.0)
     elif wl["eq"] == "OUProcessEquation":
-        eq = dpi.OUProcessEquation(nx=NX, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
+        eq = dpi.OUProcessEquation(nx=nx, T=1.0, alpha=1.0, num_components=5, mean_scale=1.0, var_scale=2.0,
                                    alpha_scale=4.0)
     else:
-        eq = dpi.GBMEquationComplexExact(NX, 1.0, 1.0)
+        eq = dpi.GBMEquationComplexExact(nx, 1.0, 1.0)
     if wl.get("pis"):
-        net = dpi.PISGradNet(hidden_shapes=wl["widths"], dim=NX, g0=eq.g, T=1.0)
+        net = dpi.PISGradNet(hidden_shapes=wl["widths"], dim=nx, g0=eq.g, T=1.0)
     else:
-        net = dpi.construct_mlp(1 + NX, 1, wl["widths"], ["ELU"] * len(wl["widths"]), None)
+        net = dpi.construct_mlp(1 + nx, 1, wl["widths"], ["ELU"] * len(wl["widths"]), None)
     return eq, net
 
 
 def _oracle_objects(wl, eq, net):
     """The CPU oracle's equation and network for a workload (fp64 numpy, oracle/dpi_oracle.py)."""
     from oracle import dpi_oracle as O
+    nx = wl.get("nx", NX)
     if wl["eq"] == "Cha":
-        oeq = O.Cha(NX, 1.0, 5.0, 1.0)
+        oeq = O.Cha(nx, 1.0, 5.0, 1.0)
     elif wl["eq"] == "OUProcessEquation":
-        oeq = O.OUProcessEquation(NX, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
+        oeq = O.OUProcessEquation(nx, eq.mean.numpy(), eq.var.numpy(), eq.pi.numpy(), alpha_scale=4.0)
     else:
-        oeq = O.GBMEquationComplexExact(NX, eq.w.numpy(), eq.v.numpy())
+        oeq = O.GBMEquationComplexExact(nx, eq.w.numpy(), eq.v.numpy())
     if wl.get("pis"):
         onet = O.PISGradNet({k: v.detach().double().numpy() for k, v in net.state_dict().items()}, oeq, T=1.0)
     else:
@@ -144,6 +152,7 @@ def live_parity(wl, eq, net, tx, pb, y, M):
     import numpy as np
     from oracle import dpi_oracle as O
     oeq, onet = _oracle_objects(wl, eq, net)
+    nx = wl.get("nx", NX)
     t0 = time.perf_counter()
     txr = tx[:1].double().cpu().numpy()
     if wl.get("hess"):
@@ -152,9 +161,9 @@ def live_parity(wl, eq, net, tx, pb, y, M):
         ref = O.labels_grad(oeq, onet, txr, M, wl["K"], 1, 1, pb, v=wl["sdgd"], m_chunk=512)
     got = y[:1].double().cpu().numpy()
     r = lambda a, b: float(np.linalg.norm(a - b) / np.linalg.norm(b))  # noqa: E731
-    out = {"value": r(got[:, :1], ref[:, :1]), "grad": r(got[:, 1:1 + NX], ref[:, 1:1 + NX])}
+    out = {"value": r(got[:, :1], ref[:, :1]), "grad": r(got[:, 1:1 + nx], ref[:, 1:1 + nx])}
     if wl.get("hess"):
-        out["hessian"] = r(got[:, 1 + NX:], ref[:, 1 + NX:])
+        out["hessian"] = r(got[:, 1 + nx:], ref[:, 1 + nx:])
     out.update(tolerance=1e-4, what=f"first point of the first timed batch (point index {pb}), {M} paths x "
                                     f"K={wl['K']} vs the fp64 oracle (oracle/dpi_oracle.py) on the same Philox counters",
                oracle_s=round(time.perf_counter() - t0, 2))
@@ -554,7 +563,7 @@ def main():
             "workload_key": args.workload,
             "data": "synthetic (Philox-sampled collocation points; random-init ELU MLP, torch.manual_seed(0))",
             "config": {"workload": wl["desc"], "baseline_config": wl["cfg"],
-                       "points": N_POINTS, "mc_paths_per_gpu": M_PER_GPU, "euler_steps": K_STEPS, "nx": NX,
+                       "points": N_POINTS, "mc_paths_per_gpu": M_PER_GPU, "euler_steps": K_STEPS, "nx": wl.get("nx", NX),
                        "parallelism": f"mc-shard{world}", "per_gpu_value": value / world,
                        "arithmetic": ("fp32 noise / Euler-Maruyama / label moments; network "
                                       + ("on exact-fp32 MFMA" if os.environ.get("DPI_GEMM", "") == "f32" else

@@ -63,7 +63,10 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 // the Hessian-label k_paths: 1 -> 4 r04o (same-box A/B, 2 pairs: 1.747 -> 1.719 ms/step)
 #define DPI_NOISE_UNROLL_HESS 4
 #endif
-constexpr int NXP_MAX = 128;       // max padded state dimension
+constexpr int NXP_MAX = 128;       // max padded state dimension of the two-workgroups-per-CU path kernels
+// max state dimension of the wide first-order instances (Cha / OU, one workgroup per CU: the noise
+// tile of 256 dims x 64 paths is 70 KB of LDS; dpi_paths_wide_*.hip)
+constexpr int NXW_MAX = 256;
 constexpr int HMAX = 128;
 
 struct NetDev {
@@ -269,16 +272,19 @@ __device__ __forceinline__ void split_rows32(const uint32_t* wsh, int C, int jj,
 #include "dpi_pis.h"
 namespace dpi {
 
-// LDS layout (floats) shared by the baseline and path kernels.
-struct Lds {
-  float S[NXP_MAX * SS];   // [dim][path] integral noise sums (path kernel) / x tile (baseline)
+// LDS layout (floats) of the first-order path kernels for state dimensions up to NXW.
+template <int NXW_>
+struct LdsT {
+  static constexpr int NXW = NXW_;
+  float S[NXW * SS];       // [dim][path] integral noise sums
   float W[2 * 32 * HMAX];  // weight chunk: f32 rows of stride WST, or two split chunks (LDS-DMA ring)
   float vec[4 * HMAX];     // base0 | w1t | wout | c1
   float bh[4 * HMAX];      // hidden-layer biases
-  float xsh[NXP_MAX];      // point x (path kernel) / zeros (baseline)
+  float xsh[NXW];          // point x
   float gst[4 * P * NSG];  // per-wave partial g statistics
   float tau[P], cmul[P], bsh[P];
 };
+using Lds = LdsT<NXP_MAX>;
 
 // ------------------------------------------------------------------------------ MLP tile
 // u and gradient terms for the 16 paths of this wave (path column pp = 16*wave + (lane&15)).
@@ -299,6 +305,49 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
   float act[L][HT][4];
 
   // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
+  if constexpr (SH::NXW > NXP_MAX) {  // wide instances: W1x staged in column blocks of 128
+#pragma unroll
+    for (int T0 = 0; T0 < HT; T0 += 2) {
+      const int nr = (HT - T0) >= 2 ? 32 : 16;
+      floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int cb = 0; 128 * cb < net.nxp; ++cb) {
+        const int ncb = min(128, net.nxp - 128 * cb), nf4 = ncb >> 2;
+        __syncthreads();
+        for (int idx = threadIdx.x; idx < nr * nf4; idx += NTH) {
+          const int r = idx / nf4, c = idx - r * nf4;
+          *reinterpret_cast<float4*>(sh.W + r * WST + 4 * c) =
+              *reinterpret_cast<const float4*>(net.W1x + (size_t)(16 * T0 + r) * net.nxp + 128 * cb + 4 * c);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int T2 = 0; T2 < 2; ++T2) {
+          if (T0 + T2 < HT) {
+            const float* wrow = sh.W + (16 * T2 + jj) * WST + 4 * qq;
+            for (int t = 0; t < (ncb >> 4); ++t) {
+              const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
+              const float* bc = sh.S + (128 * cb + 16 * t + 4 * qq) * SS + pp;
+              acc[T2] = mfma4(a.x, bc[0], acc[T2]);
+              acc[T2] = mfma4(a.y, bc[SS], acc[T2]);
+              acc[T2] = mfma4(a.z, bc[2 * SS], acc[T2]);
+              acc[T2] = mfma4(a.w, bc[3 * SS], acc[T2]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int T2 = 0; T2 < 2; ++T2) {
+        const int T = T0 + T2;
+        if (T < HT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = 16 * T + 4 * qq + r;
+            const float z = fmaf(cm, acc[T2][r], fmaf(sh.vec[H + h], tau, sh.vec[h]));
+            act[0][T][r] = Act<ACT>::f(z);
+          }
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int T0 = 0; T0 < HT; T0 += 2) {
     const int nr = (HT - T0) >= 2 ? 32 : 16;
@@ -328,6 +377,7 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
         }
       }
     }
+  }
   }
   // ---------------- hidden layers
 #pragma unroll
@@ -454,20 +504,31 @@ __device__ __forceinline__ void mlp_tile(const EqDev& e, const NetDev& net, SH& 
 // MFMAs of the current chunk; no registers, one barrier per chunk).
 // Chunk index -> (matrix, C, row offset): layer 1 (W1x), hidden layers (W_l), backward
 // (W_{l+1}^T, l = L-2..0), then — GRAD_FULL only — the input gradient (W1x^T).
-template <int H, int L>
+// NXW > 128 (the wide instances): a layer-1 chunk of 32 rows is split into column sub-chunks of
+// 128 words (the ring slot's width), nc1 per row pair, in column order.
+template <int H, int L, int NXW = NXP_MAX>
 struct SplitStream {
   static constexpr int NT = H / 32;  // chunks per H-row matrix
+  static constexpr int NCW = NXW / 128;  // layer-1 column sub-chunks per 32-row chunk, at most
   const NetDev& net;
-  int C1, n1, nT1, total;
+  int C1, nc1, n1, nT1, total;
   __device__ SplitStream(const NetDev& n, bool grad_full) : net(n) {
     C1 = n.nxp32;
-    n1 = NT;                               // layer-1 chunks (H output rows)
+    nc1 = NCW == 1 ? 1 : (C1 + 127) >> 7;
+    n1 = NT * nc1;                         // layer-1 chunks (H output rows)
     nT1 = C1 / 32;                         // W1x^T chunks (C1 output rows)
     total = n1 + 2 * (L - 1) * NT + (grad_full ? nT1 : 0);
   }
-  __device__ __forceinline__ void desc(int idx, const uint32_t*& g, int& C, int& r0) const {
+  // chunk idx: source g (first word of its first row), LDS row width C, source row stride Cg, first row r0
+  __device__ __forceinline__ void desc(int idx, const uint32_t*& g, int& C, int& Cg, int& r0) const {
+    Cg = 0;
     if (idx < n1) {
-      g = net.W1xS, C = C1, r0 = 32 * idx;
+      if constexpr (NCW == 1) {
+        g = net.W1xS, C = C1, r0 = 32 * idx;
+      } else {
+        const int pr = idx / nc1, kc = idx - pr * nc1;
+        g = net.W1xS + 128 * kc, C = min(128, C1 - 128 * kc), Cg = C1, r0 = 32 * pr;
+      }
       return;
     }
     idx -= n1;
@@ -483,19 +544,24 @@ struct SplitStream {
     idx -= (L - 1) * NT;
     g = net.W1xTS, C = H, r0 = 32 * idx;
   }
+  __device__ __forceinline__ void desc(int idx, const uint32_t*& g, int& C, int& r0) const {
+    int Cg;
+    desc(idx, g, C, Cg, r0);
+  }
   // LDS-DMA of chunk idx into ring slot idx & 1: wave-instruction w writes LDS granules
   // [64 w, 64 w + 64) lane-linearly; lane i's source is the granule that belongs there.
   __device__ __forceinline__ void issue(int idx, uint32_t* ring) const {
     if (idx >= total) return;
     const uint32_t* g;
-    int C, r0;
-    desc(idx, g, C, r0);
+    int C, Cg, r0;
+    desc(idx, g, C, Cg, r0);
+    if (NCW == 1 || Cg == 0) Cg = C;
     uint32_t* dst = ring + (idx & 1) * (32 * HMAX);
     const int gpr = C >> 2, m = split_swz(C), lane = threadIdx.x & 63;
     for (int w = threadIdx.x >> 6; w < (C >> 3); w += NTH / 64) {
       const int G = 64 * w + lane, r = G / gpr, gs = (G - r * gpr) ^ (r & m);
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(g + (size_t)(r0 + r) * C + 4 * gs),
+          (const __attribute__((address_space(1))) void*)(g + (size_t)(r0 + r) * Cg + 4 * gs),
           (__attribute__((address_space(3))) void*)(dst + 256 * w), 16, 0, 0);
     }
   }
@@ -525,7 +591,8 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   const float tau = sh.tau[pp];
   const float cm = sh.cmul[pp];
   uint32_t* wsh = reinterpret_cast<uint32_t*>(sh.W);
-  SplitStream<H, L> ss(net, Eq<KIND>::GRAD_FULL);
+  constexpr int NXW = SH::NXW;
+  SplitStream<H, L, NXW> ss(net, Eq<KIND>::GRAD_FULL);
   const int nu1 = ss.C1 >> 5;
   int chunk = 0;
   ss.issue(0, wsh);
@@ -533,9 +600,9 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   half8 bh[NU], bl[NU];
 
   // ---------------- layer 1: z = base0 + w1t*tau + cmul * (W1x S)
-  half8 xh[NXP_MAX / 32], xl[NXP_MAX / 32];  // the noise tile as B operand, split once
+  half8 xh[NXW / 32], xl[NXW / 32];  // the noise tile as B operand, split once
 #pragma unroll
-  for (int u = 0; u < NXP_MAX / 32; ++u) {
+  for (int u = 0; u < NXW / 32; ++u) {
     float x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = u < nu1 ? sh.S[(32 * u + 4 * qq + (j & 3) + 16 * (j >> 2)) * SS + pp] : 0.f;
@@ -543,21 +610,26 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
   }
 #pragma unroll
   for (int T0 = 0; T0 < HT; T0 += 2) {
-    int C;
-    const uint32_t* wch = ss.enter(chunk++, wsh, C);
     floatx4 am[2], ac[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) am[t] = ac[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < NXP_MAX / 32; ++u) {
-      if (u < nu1) {
+    for (int kc = 0; kc < NXW / 128; ++kc) {  // column sub-chunks of 128 words (one for NXW = 128)
+      if (kc == 0 || 128 * kc < ss.C1) {
+        int C;
+        const uint32_t* wch = ss.enter(chunk++, wsh, C);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          half8 ah, al;
-          load_a_split(wch, C, 16 * t + jj, u, qq, ah, al);
-          am[t] = mfma16(ah, xh[u], am[t]);
-          ac[t] = mfma16(ah, xl[u], ac[t]);
-          ac[t] = mfma16(al, xh[u], ac[t]);
+        for (int u = 0; u < 4; ++u) {
+          if (4 * kc + u < nu1) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              half8 ah, al;
+              load_a_split(wch, C, 16 * t + jj, u, qq, ah, al);
+              am[t] = mfma16(ah, xh[4 * kc + u], am[t]);
+              ac[t] = mfma16(ah, xl[4 * kc + u], ac[t]);
+              ac[t] = mfma16(al, xh[4 * kc + u], ac[t]);
+            }
+          }
         }
       }
     }
@@ -655,6 +727,7 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
 // 100-direction tangent sweep.  H <= 64, L <= 4.
 template <int H>
 struct LdsGbm {
+  static constexpr int NXW = NXP_MAX;
   static constexpr int WXS = NXP_MAX + 8;  // W1x row stride (WXS/4 = 2 mod 4)
   static constexpr int WHS = H + 8;        // hidden row stride
   float S[NXP_MAX * SS];
@@ -1241,21 +1314,25 @@ __device__ __forceinline__ float base_matvec(const float* __restrict__ Wt, const
   const int tid = threadIdx.x;
   const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NT / G4;
   const int kc = (K + ns - 1) / ns, k0 = sl * kc;
-  float4 w[KCM];
-#pragma unroll
-  for (int j = 0; j < KCM; ++j)  // all loads in flight
-    w[j] = (j < kc && k0 + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + j) * H + 4 * g)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
   float a[4] = {0.f, 0.f, 0.f, 0.f};
+  // passes of KCM k per slice: one for every K <= 128 (every mat-vec but a wide layer 1, nx up to
+  // NXW_MAX, which takes two), the slice's k in order either way
+  for (int kb = 0; kb < kc; kb += KCM) {
+    float4 w[KCM];
 #pragma unroll
-  for (int j = 0; j < KCM; ++j)
-    if (j < kc && k0 + j < K) {
-      const float vk = v[k0 + j];
-      a[0] = fmaf(w[j].x, vk, a[0]);
-      a[1] = fmaf(w[j].y, vk, a[1]);
-      a[2] = fmaf(w[j].z, vk, a[2]);
-      a[3] = fmaf(w[j].w, vk, a[3]);
-    }
+    for (int j = 0; j < KCM; ++j)  // all loads in flight
+      w[j] = (kb + j < kc && k0 + kb + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + kb + j) * H + 4 * g)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < KCM; ++j)
+      if (kb + j < kc && k0 + kb + j < K) {
+        const float vk = v[k0 + kb + j];
+        a[0] = fmaf(w[j].x, vk, a[0]);
+        a[1] = fmaf(w[j].y, vk, a[1]);
+        a[2] = fmaf(w[j].z, vk, a[2]);
+        a[3] = fmaf(w[j].w, vk, a[3]);
+      }
+  }
   // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
   for (int o = G4; o < 64; o <<= 1)
 #pragma unroll
@@ -1274,7 +1351,7 @@ __device__ __forceinline__ float base_matvec(const float* __restrict__ Wt, const
 template <int NT>
 struct BaseLds {
   __attribute__((aligned(16))) float part[NT / 64][HMAX];
-  float xs[NXP_MAX];
+  float xs[NXW_MAX];
   float act[4][HMAX];
   float dbuf[2][HMAX];
   float red[NT / 64];
@@ -1321,13 +1398,12 @@ __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, co
         if (d < nx) row[1 + d] = x[q];
         bs.xs[d] = d < nx ? x[q] : 0.f;
       }
-    } else if (4 * nb <= tid && tid < NXP_MAX) {
-      bs.xs[tid] = 0.f;
     }
+    for (int d = 4 * nb + tid; d < NXW_MAX; d += NT) bs.xs[d] = 0.f;
   } else {
     const float* row = tx + (size_t)i * F;
     if (tid == 0) bs.ts = row[0];
-    if (tid < NXP_MAX) bs.xs[tid] = tid < nx ? row[1 + tid] : 0.f;
+    for (int d = tid; d < NXW_MAX; d += NT) bs.xs[d] = d < nx ? row[1 + d] : 0.f;
   }
   __syncthreads();
   const float t = bs.ts;
@@ -2071,18 +2147,23 @@ __device__ __forceinline__ void fused_reduce(const PathArgs& a, int i, int F, co
 // Two workgroups per CU (256 registers per wave) except GBM / TD (one: their LDS) and the exact-fp32
 // OU 4 x 128 instance — the range guard's fallback for OU MLP nets — whose GMM statistics beside
 // the 128 fp32 activation registers spilled 4 VGPRs at 256: it runs at one workgroup per CU instead.
-template <int KIND, int H, int L, bool SPLIT, bool TD>
+// Wide instances (NXW > NXP_MAX): one (their 70 KB noise tile).
+template <int KIND, int H, int L, bool SPLIT, bool TD, int NXW = NXP_MAX>
 constexpr int k_paths_wgs() {
-  return (KIND == DPI_EQ_GBM || TD || (KIND == DPI_EQ_OU && !SPLIT && H == 128 && L == 4)) ? 1 : 2;
+  return (KIND == DPI_EQ_GBM || TD || NXW > NXP_MAX || (KIND == DPI_EQ_OU && !SPLIT && H == 128 && L == 4)) ? 1 : 2;
 }
 // The path launch body; FBT: the one-launch sample_with_gradients form (k_paths_fb), whose first
 // fb.nbase blocks are the points' base blocks — a kernel of its own, so the plain k_paths keeps its
 // register allocation (the hand-off's arguments live across the whole kernel).
-template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS, bool TD, int ACT, bool FBT>
+// NXW: the state-dimension cap of the instance (NXP_MAX; NXW_MAX for the wide first-order instances)
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS, bool TD, int ACT, bool FBT, int NXW = NXP_MAX>
 __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, const PathArgs& a, const FusedBase& fb) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
-  using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, Lds>;
+  static_assert(NXW == NXP_MAX || (KIND != DPI_EQ_GBM && !HESS && !FBT && NXW % 128 == 0 && NXW <= NXW_MAX),
+                "wide instances: first-order Cha / OU labels, no fused baseline");
+  using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, LdsT<NXW>>;
+  constexpr int NBW = NXW / 16;  // dim-blocks of 4 per wave (4 waves)
   __shared__ SH sh;
   constexpr bool GBM = KIND == DPI_EQ_GBM;
   // fused baseline (k_paths_fb): the first fb.nbase blocks are the points' base blocks
@@ -2206,7 +2287,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   __syncthreads();  // xsh ready
 
   // ---------------- phase 1: K-step Euler–Maruyama rollouts
-  float ST[8][4];
+  float ST[NBW][4];
   float gst[NSG], fst[NSG];
 #pragma unroll
   for (int c = 0; c < NSG; ++c) gst[c] = fst[c] = 0.f;
@@ -2231,7 +2312,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   }
   auto terminal_rollout = [&]() {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NBW; ++c) {
       const int j = wv + 4 * c;  // terminal dim-blocks of this wave
       ST[c][0] = ST[c][1] = ST[c][2] = ST[c][3] = 0.f;
       if (TERM && j < nb) {
@@ -2264,7 +2345,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   };
   auto integral_rollout = [&]() {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NBW; ++c) {
       const int j = (3 - wv) + 4 * c;  // integral dim-blocks of this wave (balances 13/12/12/13)
       if (j < nb) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -2395,7 +2476,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   // TD terminal value u(t_next, x + cT S_T) (data.py:941-942), per lane = path
   [[maybe_unused]] auto terminal_value_td = [&]() -> float {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NBW; ++c) {
       const int j = wv + 4 * c;
       if (j < nb)
 #pragma unroll
@@ -2491,53 +2572,90 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   // per-block sums of c and c^2 for this wave's columns: 2 per owned dim (d = 4 (wv + 4c) + q,
   // column 8c + 2q + {0: sum, 1: sum of squares}) and, on wave 0, the value column (56, 57)
   const float aY = ap * yT, bY = bp * yI;
-  float col[64];
-#pragma unroll
-  for (int c = 0; c < 64; ++c) col[c] = 0.f;
-#pragma unroll
-  for (int c = 0; c < 7; ++c) {
-    const int j = wv + 4 * c;
-    if (j < nb) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int d = 4 * j + q;
-        const float v = d < nx ? fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]) : 0.f;
-        col[8 * c + 2 * q] = v;
-        col[8 * c + 2 * q + 1] = v * v;
+  if constexpr (NXW == NXP_MAX) {
+    float col[64];
+  #pragma unroll
+    for (int c = 0; c < 64; ++c) col[c] = 0.f;
+  #pragma unroll
+    for (int c = 0; c < 7; ++c) {
+      const int j = wv + 4 * c;
+      if (j < nb) {
+  #pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int d = 4 * j + q;
+          const float v = d < nx ? fmaf(aY, ST[c][q], bY * sh.S[d * SS + lane]) : 0.f;
+          col[8 * c + 2 * q] = v;
+          col[8 * c + 2 * q + 1] = v * v;
+        }
       }
     }
-  }
-  if (wv == 0) {
-    float fbt;
-    if constexpr (GBM)
-      fbt = sh.fbp[lane];
-    else
-      fbt = f_b + Eq<KIND>::ffc(e);
-    const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
-    col[56] = c0;
-    col[57] = c0 * c0;
-  }
-  const float tot = column_sums64(col);
-  {
-    const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
-    const int d = 4 * (wv + 4 * c) + q;
-    if (lane < 56) {
-      if (wv + 4 * c < nb && d < nx) out[sq * F + 1 + d] = tot;
-    } else if (wv == 0 && lane < 58) {
-      out[sq * F] = tot;
+    if (wv == 0) {
+      float fbt;
+      if constexpr (GBM)
+        fbt = sh.fbp[lane];
+      else
+        fbt = f_b + Eq<KIND>::ffc(e);
+      const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
+      col[56] = c0;
+      col[57] = c0 * c0;
     }
-  }
-  if (wv + 28 < nb) {  // nx > 112: the eighth dim-block of this wave, one column at a time
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int d = 4 * (wv + 28) + q;
-      if (d < nx) {
-        const float v = fmaf(aY, ST[7][q], bY * sh.S[d * SS + lane]);
-        const float s1 = wave_sum(v), s2 = wave_sum(v * v);
-        if (lane == 0) {
-          out[1 + d] = s1;
-          out[F + 1 + d] = s2;
+    const float tot = column_sums64(col);
+    {
+      const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
+      const int d = 4 * (wv + 4 * c) + q;
+      if (lane < 56) {
+        if (wv + 4 * c < nb && d < nx) out[sq * F + 1 + d] = tot;
+      } else if (wv == 0 && lane < 58) {
+        out[sq * F] = tot;
+      }
+    }
+    if (wv + 28 < nb) {  // nx > 112: the eighth dim-block of this wave, one column at a time
+  #pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int d = 4 * (wv + 28) + q;
+        if (d < nx) {
+          const float v = fmaf(aY, ST[7][q], bY * sh.S[d * SS + lane]);
+          const float s1 = wave_sum(v), s2 = wave_sum(v * v);
+          if (lane == 0) {
+            out[1 + d] = s1;
+            out[F + 1 + d] = s2;
+          }
         }
+      }
+    }
+  } else {
+    // wide instances: this wave's NBW dim-blocks in groups of 7 (56 columns), the value column with
+    // the first group; one column_sums64 per group
+#pragma unroll
+    for (int g0 = 0; g0 < NBW; g0 += 7) {
+      float col[64];
+#pragma unroll
+      for (int c = 0; c < 64; ++c) col[c] = 0.f;
+#pragma unroll
+      for (int c = 0; c < 7; ++c) {
+        const int j = wv + 4 * (g0 + c);
+        if (g0 + c < NBW && j < nb) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int d = 4 * j + q;
+            const float v = d < nx ? fmaf(aY, ST[g0 + c < NBW ? g0 + c : 0][q], bY * sh.S[d * SS + lane]) : 0.f;
+            col[8 * c + 2 * q] = v;
+            col[8 * c + 2 * q + 1] = v * v;
+          }
+        }
+      }
+      if (g0 == 0 && wv == 0) {
+        const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
+        col[56] = c0;
+        col[57] = c0 * c0;
+      }
+      const float tot = column_sums64(col);
+      const int c = lane >> 3, q = (lane >> 1) & 3, sq = lane & 1;
+      const int j = wv + 4 * (g0 + c), d = 4 * j + q;
+      if (lane < 56) {
+        if (g0 + c < NBW && j < nb && d < nx) out[sq * F + 1 + d] = tot;
+      } else if (g0 == 0 && wv == 0 && lane < 58) {
+        out[sq * F] = tot;
       }
     }
   }
@@ -2548,9 +2666,10 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   }
 }
 
-template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU>
-__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD>())) void k_paths(EqDev e, NetDev net, PathArgs a) {
-  paths_body<KIND, H, L, ZERO, SPLIT, HESS, TD, ACT, false>(e, net, a, FusedBase{});
+template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS = false, bool TD = false, int ACT = DPI_ACT_ELU,
+          int NXW = NXP_MAX>
+__global__ __launch_bounds__(256, (k_paths_wgs<KIND, H, L, SPLIT, TD, NXW>())) void k_paths(EqDev e, NetDev net, PathArgs a) {
+  paths_body<KIND, H, L, ZERO, SPLIT, HESS, TD, ACT, false, NXW>(e, net, a, FusedBase{});
 }
 // The one-launch dpi_sample_with_gradients: fb.nbase base blocks ahead of the path blocks.
 template <int KIND, int H, int L, bool ZERO, bool SPLIT, int ACT = DPI_ACT_ELU>

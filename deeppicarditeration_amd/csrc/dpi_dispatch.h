@@ -68,9 +68,20 @@ template <int KIND, int H, int L, bool Z, int ACT>
 constexpr bool fused_base_shape() {
   return KIND != DPI_EQ_GBM && ACT == DPI_ACT_ELU && (Z || (H % 32 == 0 && !(KIND == DPI_EQ_OU && H == 128 && L == 4)));
 }
-template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU, bool FBV = false>
+// NXW > NXP_MAX: the wide first-order instances (Cha / OU, nx up to NXW_MAX; dpi_paths_wide_*.hip):
+// plain k_paths only — the baseline is shape-generic, the TD / Hessian / fused-baseline forms have none.
+template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU, bool FBV = false, int NXW = NXP_MAX>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
-  if constexpr (FBV) {
+  if constexpr (NXW > NXP_MAX) {
+    static_assert(KIND != DPI_EQ_GBM && !TDV && !FBV, "wide instances: first-order Cha / OU");
+    if constexpr (!Z && H % 32 == 0) {
+      if (q.a->split) {
+        DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, true, false, false, ACT, NXW>), q, p->e, net->d, *q.a);
+        return;
+      }
+    }
+    DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, false, false, false, ACT, NXW>), q, p->e, net->d, *q.a);
+  } else if constexpr (FBV) {
     if constexpr (fused_base_shape<KIND, H, L, Z, ACT>())
       DPI_PATH_LAUNCH((k_paths_fb<KIND, H, L, Z, !Z, ACT>), q, p->e, net->d, *q.a,
                          *q.fbase);
@@ -116,18 +127,21 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
                        net->d, *q.a);
 }
 
-template <int KIND, bool TDV = false, int ACT = DPI_ACT_ELU, bool FBV = false>
+template <int KIND, bool TDV = false, int ACT = DPI_ACT_ELU, bool FBV = false, int NXW = NXP_MAX>
 bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
+  if constexpr (NXW > NXP_MAX) {
+    if (q.baseline || q.hess || q.fbase) return false;
+  }
   if constexpr (ACT == DPI_ACT_ELU) {  // zero nets and the (activation-generic) baseline: the ELU units
     if (net->d.kind == 0) {
-      do_launch<KIND, 16, 1, true, TDV, DPI_ACT_ELU, FBV>(p, net, q);
+      do_launch<KIND, 16, 1, true, TDV, DPI_ACT_ELU, FBV, NXW>(p, net, q);
       return true;
     }
   } else {
     if (net->d.kind == 0 || q.baseline) return false;
   }
   const int H = net->d.H, L = net->d.L;
-  if constexpr (!TDV && !FBV && ACT == DPI_ACT_ELU) {
+  if constexpr (!TDV && !FBV && ACT == DPI_ACT_ELU && NXW == NXP_MAX) {
     if (q.baseline) {  // the baseline kernel is shape-generic
       if (KIND == DPI_EQ_GBM && H > 64) return false;
       do_launch<KIND, 16, 1, false, false>(p, net, q);
@@ -137,7 +151,7 @@ bool dpi_dispatch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q)
   if constexpr (KIND == DPI_EQ_GBM) {  // all weights LDS-resident: H <= 64
 #define DPI_SHAPE(HH, LL)                      \
   if (H == HH && L == LL) {                    \
-    do_launch<KIND, HH, LL, false, TDV, ACT, FBV>(p, net, q); \
+    do_launch<KIND, HH, LL, false, TDV, ACT, FBV, NXW>(p, net, q); \
     return true;                               \
   }
     DPI_SHAPE(64, 3)
@@ -177,3 +191,7 @@ bool dispatch_td_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Lau
 bool dispatch_td_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_fb_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_fb_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

@@ -552,7 +552,7 @@ static dpi_problem_s* new_problem(int kind, int nx, double alpha, double T) {
 }
 
 int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out) {
-  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "cha: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (nx > NXW_MAX) return fail(DPI_ERR_UNSUPPORTED, "cha: nx exceeds the compiled maximum state dimension 256 (NXW_MAX)");
   if (!out || nx < 1 || !(alpha > 0)) return fail(DPI_ERR_ARG, "cha: bad arguments");
   auto* p = new_problem(DPI_EQ_CHA, nx, alpha, T);
   const double kp = k / std::sqrt((double)nx);  // equations.py:285
@@ -565,9 +565,9 @@ int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem
 
 int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale, int n_comp,
                           const double* mean, const double* var_diag, const double* pi, dpi_problem* out) {
-  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "ou: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (nx > NXW_MAX) return fail(DPI_ERR_UNSUPPORTED, "ou: nx exceeds the compiled maximum state dimension 256 (NXW_MAX)");
   if (!out || nx < 1 || n_comp < 1 || n_comp > NSG || !mean || !var_diag || !pi)
-    return fail(DPI_ERR_ARG, "ou: bad arguments (1 <= n_comp <= 8, nx <= 128)");
+    return fail(DPI_ERR_ARG, "ou: bad arguments (1 <= n_comp <= 8, nx <= 256)");
   auto* p = new_problem(DPI_EQ_OU, nx, alpha, T);
   p->e.ou_theta = (float)theta;
   p->e.ou_mu = (float)mu;
@@ -713,8 +713,8 @@ int dpi_net_status_peek(dpi_net net, int slot, int* status) {
 
 int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const float* params, size_t n_params,
                        dpi_net* out) {
-  if (n_in - 1 > NXP_MAX)
-    return fail(DPI_ERR_UNSUPPORTED, "mlp: nx = n_in - 1 exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (n_in - 1 > NXW_MAX)
+    return fail(DPI_ERR_UNSUPPORTED, "mlp: nx = n_in - 1 exceeds the compiled maximum state dimension 256 (NXW_MAX)");
   if (!out || !widths || !params || n_in < 2 || n_hidden < 1 || n_hidden > 4)
     return fail(DPI_ERR_ARG, "mlp: bad arguments");
   if (act != DPI_ACT_ELU && act != DPI_ACT_TANH)
@@ -1579,6 +1579,18 @@ static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Lau
     }
   }
   const bool td = q.td && !q.baseline && !q.hess;
+  if (p->e.nx > NXP_MAX && !q.baseline) {  // the wide first-order units (nx <= NXW_MAX; Cha / OU)
+    if (td || q.hess) return false;
+    const bool tanh = net->d.kind == 1 && net->d.act == DPI_ACT_TANH;
+    switch (p->e.kind) {
+      case DPI_EQ_CHA:
+        return tanh ? dispatch_wide_cha_tanh(p, net, q) : dispatch_wide_cha(p, net, q);
+      case DPI_EQ_OU:
+        return tanh ? dispatch_wide_ou_tanh(p, net, q) : dispatch_wide_ou(p, net, q);
+      default:
+        return false;
+    }
+  }
   if (net->d.kind == 1 && net->d.act == DPI_ACT_TANH && !q.baseline) {  // the Tanh k_paths units
     switch (p->e.kind) {
       case DPI_EQ_CHA:
@@ -1608,7 +1620,9 @@ extern "C" {
 static int check_pair(dpi_problem p, dpi_net net) {
   if (!p || !net) return fail(DPI_ERR_ARG, "null problem or net");
   if (net->d.kind && net->n_in != 1 + p->e.nx) return fail(DPI_ERR_ARG, "net input width != 1 + nx");
-  if (net->d.kind && net->d.nxp > NXP_MAX) return fail(DPI_ERR_ARG, "nx too large");
+  if (net->d.kind && net->d.nxp > NXW_MAX) return fail(DPI_ERR_ARG, "nx too large");
+  if (p->e.nx > NXP_MAX && net->d.kind == 2)
+    return fail(DPI_ERR_UNSUPPORTED, "PISGradNet: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
   return 0;
 }
 
@@ -1879,6 +1893,9 @@ static int moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int 
   } else {
     Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
     q.td = p->td_dt > 0.f;
+    if (q.td && p->e.nx > NXP_MAX)
+      return fail(DPI_ERR_UNSUPPORTED, "label_moments: the TD estimators (ESTIMATE_DELTA_T > 0) are compiled for "
+                                       "nx <= 128 (NXP_MAX)");
     take_timer(q.t0, q.t1);
     if ((flags & DPI_PREPARED) && stages_prepare(p, net)) a.noise = (const float*)(b + w.noise);
     if (nbp <= 64 && fused_reduce_on()) {  // k_paths' last block per point reduces and finalizes
@@ -1917,7 +1934,7 @@ static bool fused_base_on() {
 // first-order Cha / OU labels without TD, of zero nets or ELU MLP nets in the fp16-split mode
 // (H % 32 == 0, the fused-MLP instances; not OU 4 x 128); the rest runs the two-launch form.
 static bool fused_base_ok(dpi_problem p, dpi_net net) {
-  if (p->e.kind == DPI_EQ_GBM || p->td_dt > 0.f) return false;
+  if (p->e.kind == DPI_EQ_GBM || p->td_dt > 0.f || p->e.nx > NXP_MAX) return false;
   if (net->d.kind == 0) return true;
   const int H = net->d.H, L = net->d.L;
   return net->d.kind == 1 && net->d.act == DPI_ACT_ELU && H % 32 == 0 && mlp_split(net) &&

@@ -21,6 +21,8 @@ The data module keeps its code paths:
 
 The reference itself is never imported here; `base` is whatever class the caller passes.
 """
+import warnings
+
 import torch
 
 from .data import OnlineDataGenerator
@@ -54,6 +56,10 @@ def _cfg_get(cfg, key, default):
     return default if v is None else v
 
 
+class HipWorkersNote(UserWarning):
+    """DATA.N_WORKERS > 0 under DATA.BACKEND hip: the loader runs without worker processes."""
+
+
 def hip_online_data_generator(kws, data_cfg=None, base=None, generator_cls=None):
     """The HIP generator for the `kws` PicardDataModule.get_data_generator builds (data.py:1474-1488:
     equation, solution, N, i, device, **DATA.kwargs, hessian_approximation, sample_bound,
@@ -70,12 +76,13 @@ def hip_online_data_generator(kws, data_cfg=None, base=None, generator_cls=None)
     cap = int(_cfg_get(data_cfg, "POINTS_PER_CALL", DEFAULT_POINTS_PER_CALL))
     workers = [int(_cfg_get(data_cfg, k, 0) or 0) for k in ("N_WORKERS", "PRELOAD_N_WORKERS")]
     if max(workers) > 0:
-        # the reference's default is DATA.N_WORKERS 1 (picard/config.py:75): its DataLoader would then
-        # pickle the dataset into spawned worker processes (data.py:1542-1549, 1768-1779), and the
-        # HIP generator's problem / network handles are device state of this process
-        raise ValueError(f"DATA.BACKEND hip labels in the training process itself (one fused kernel per call, "
-                         f"no DataLoader workers): set DATA.N_WORKERS 0 (got N_WORKERS {workers[0]}, "
-                         f"PRELOAD_N_WORKERS {workers[1]}); every shipped DPI YAML sets N_WORKERS: 0")
+        # the reference's default is DATA.N_WORKERS 1 (picard/config.py:75): its DataLoader would run the
+        # dataset in worker processes (data.py:1768-1779).  The HIP labels come from one fused kernel per
+        # call on this process's stream (device handles of this process), so the patched
+        # train_dataloader builds the loader with no workers for DATA.BACKEND hip; the batches are the
+        # ones N_WORKERS 0 draws (counter-based noise: worker processes would only move them)
+        warnings.warn(f"DATA.BACKEND hip labels in the training process: DATA.N_WORKERS {workers[0]} "
+                      f"(PRELOAD_N_WORKERS {workers[1]}) runs as N_WORKERS 0", HipWorkersNote, stacklevel=2)
     data_size = _cfg_get(data_cfg, "DATA_SIZE", None)
     n_buffer = _cfg_get(data_cfg, "N_BUFFER", None)
     if data_cfg is not None and not _cfg_get(data_cfg, "NEW_SAMPLING", False) and n_buffer in (None, 0) \

@@ -336,6 +336,18 @@ def main(only=None):
              2, 64, 2, 56, workdir=wd, hessians=True)
     run_case("td_cha_mlp32_tanh_K2", "Cha", cha, "mlp", {"neurons": [32, 32], "act": "Tanh"}, 6, 64, 2, 57,
              workdir=wd, delta_t=0.35)
+    # state dimensions above 128 (the wide first-order instances, nx <= 256; equations.py takes any nx)
+    cha200 = {**cha, "nx": 200}
+    cha256 = {**cha, "nx": 256}
+    run_case("wide_cha200_mlp64x3_K2", "Cha", cha200, "mlp", {"neurons": [64] * 3}, 2, 64, 2, 81, workdir=wd)
+    run_case("wide_cha256_mlp128x4_tanh_K2", "Cha", cha256, "mlp", {"neurons": [128] * 4, "act": "Tanh"}, 2, 64, 2,
+             82, epoch=1, workdir=wd)
+    run_case("wide_cha256_mlp16_K2", "Cha", cha256, "mlp", {"neurons": [16, 16]}, 2, 64, 2, 83, workdir=wd)
+    run_case("wide_cha256_zero_K1", "Cha", cha256, "mlp", {"neurons": [8]}, 2, 64, 1, 84, workdir=wd, zero=True)
+    run_case("wide_ou200_mlp32x2_K2", "OUProcessEquation", {**ou, "nx": 200}, "mlp", {"neurons": [32, 32]}, 2, 64, 2,
+             85, workdir=wd)
+    run_case("wide_ou256_mlp128x4_K2", "OUProcessEquation", {**ou, "nx": 256}, "mlp", {"neurons": [128] * 4}, 2, 64,
+             2, 86, workdir=wd)
     shutil.rmtree(wd)
 
 

@@ -11,9 +11,13 @@ def product_equation(f):
     if eq == "Cha":
         return dpi.Cha(int(f["eqkw_nx"]), float(f["eqkw_alpha"]), float(f["eqkw_k"]), float(f["eqkw_T"]))
     if eq == "OUProcessEquation":
+        # the reference ships its GMM files for nx = 100 only; at other nx it drew new parameters
+        # (equations.py:533-544), which the fixture holds
+        gmm = {} if int(f["eqkw_nx"]) == 100 else dict(mean=f["gmm_mean"], var=f["gmm_var"], pi=f["gmm_pi"])
         e = dpi.OUProcessEquation(nx=int(f["eqkw_nx"]), T=float(f["eqkw_T"]), alpha=float(f["eqkw_alpha"]),
                                   num_components=int(f["eqkw_num_components"]), mean_scale=float(f["eqkw_mean_scale"]),
-                                  var_scale=float(f["eqkw_var_scale"]), alpha_scale=float(f["eqkw_alpha_scale"]))
+                                  var_scale=float(f["eqkw_var_scale"]), alpha_scale=float(f["eqkw_alpha_scale"]),
+                                  **gmm)
         assert np.allclose(e.mean.numpy(), f["gmm_mean"]) and np.allclose(e.pi.numpy(), f["gmm_pi"])
         return e
     if eq == "GBMEquationComplexExact":

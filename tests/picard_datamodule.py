@@ -306,9 +306,8 @@ class PicardDataModuleStandIn:
         return dataset
 
     def train_dataloader(self):
-        """data.py:1762-1780 (N_WORKERS 0)."""
+        """data.py:1762-1780 as patched: DATA.BACKEND hip builds the loader without worker processes."""
         dataset = self.wrap_dataset(self.get_dataset_and_set_data_info())
-        assert self.data_cfg.N_WORKERS == 0
         self.initialize_dataset(dataset, 0, 1)
         return DataLoader(dataset, batch_size=None if self.data_generator.do_internal_batching else self.batch_size,
                           num_workers=0)
