@@ -2228,7 +2228,8 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   } else {
     for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
   }
-  const int nxpz = (nxp + 31) & ~31;  // the split MLP reads 32-row chunks
+  // the split MLP reads the tile's first nxp32 rows (32-row chunks, 96 padded to 128)
+  const int nxpz = ZERO ? ((nxp + 31) & ~31) : max((nxp + 31) & ~31, net.nxp32);
   for (int idx = tid; idx < (nxpz - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
     const int d = 4 * nb + idx / P, p = idx % P;
     sh.S[d * SS + p] = 0.f;

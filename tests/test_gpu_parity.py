@@ -239,9 +239,10 @@ def test_tiny_s_minus_t_regression(net_kind):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
-@pytest.mark.parametrize("nx", [1, 7, 113, 128])
+@pytest.mark.parametrize("nx", [1, 7, 80, 96, 113, 128])
 def test_dimension_edges_vs_oracle(nx, mlp_precision):
-    """Ragged and maximal state dimensions: a partial last 4-dim block (7, 113), the 8th block of
+    """Ragged and maximal state dimensions: a partial last 4-dim block (7, 113), a split layer-1 row of
+    three 32-column chunks (80, 96: padded to four, the LDS swizzle needs 1, 2 or 4), the 8th block of
     a wave (nx > 112 takes the per-column reduction path) and nx = NXP_MAX = 128."""
     import deeppicarditeration_amd as dpi
     eq = dpi.Cha(nx, 1.0, 5.0, 1.0)
