@@ -326,9 +326,11 @@ def main():
             capture.update(tx=tx_, pb=pb_, y=y)
         return y
 
-    # The timed launch of every EV_EVERY-th step (timer events on a dispatch packet are cheap, but
-    # the stop event's completion signal still makes the launch's end visible to the host)
-    EV_EVERY = 4
+    # Every step's path launch is timed: events on the dispatch packet itself add no packets between
+    # launches (same-box A/B, profiles/r06i_ab), and averaging all of them makes kernel_ms the mean
+    # launch time of the timed steps, never above ms_per_step (the launches of one stream run in
+    # order).  Slots wrap at DPI_LAUNCH_TIMERS: a run of more steps reads each slot's latest launch.
+    EV_EVERY = 1
     nstep = [0]
 
     def step():
