@@ -326,11 +326,10 @@ def main():
             capture.update(tx=tx_, pb=pb_, y=y)
         return y
 
-    # Every step's path launch is timed: events on the dispatch packet itself add no packets between
-    # launches (same-box A/B, profiles/r06i_ab), and averaging all of them makes kernel_ms the mean
-    # launch time of the timed steps, never above ms_per_step (the launches of one stream run in
-    # order).  Slots wrap at DPI_LAUNCH_TIMERS: a run of more steps reads each slot's latest launch.
-    EV_EVERY = 1
+    # The path launch of every EV_EVERY-th step is timed: events on the dispatch packet at that rate
+    # cost nothing measurable (same-box A/B, profiles/r06i_ab), while timing every launch added
+    # 8-35 us per step (r06k)
+    EV_EVERY = 4
     nstep = [0]
 
     def step():

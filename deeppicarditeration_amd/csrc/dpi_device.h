@@ -1314,13 +1314,46 @@ __device__ __forceinline__ float base_matvec(const float* __restrict__ Wt, const
   const int tid = threadIdx.x;
   const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NT / G4;
   const int kc = (K + ns - 1) / ns, k0 = sl * kc;
+  float4 w[KCM];
+#pragma unroll
+  for (int j = 0; j < KCM; ++j)  // all loads in flight
+    w[j] = (j < kc && k0 + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + j) * H + 4 * g)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
   float a[4] = {0.f, 0.f, 0.f, 0.f};
-  // passes of KCM k per slice: one for every K <= 128 (every mat-vec but a wide layer 1, nx up to
-  // NXW_MAX, which takes two), the slice's k in order either way
+#pragma unroll
+  for (int j = 0; j < KCM; ++j)
+    if (j < kc && k0 + j < K) {
+      const float vk = v[k0 + j];
+      a[0] = fmaf(w[j].x, vk, a[0]);
+      a[1] = fmaf(w[j].y, vk, a[1]);
+      a[2] = fmaf(w[j].z, vk, a[2]);
+      a[3] = fmaf(w[j].w, vk, a[3]);
+    }
+  // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
+  for (int o = G4; o < 64; o <<= 1)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] += __shfl_xor(a[r], o, 64);
+  if ((tid & 63) < G4) *reinterpret_cast<float4*>(&part[tid >> 6][4 * g]) = make_float4(a[0], a[1], a[2], a[3]);
+  __syncthreads();
+  float y = 0.f;
+  if (tid < H)
+#pragma unroll
+    for (int j = 0; j < NT / 64; ++j) y += part[j][tid];
+  return y;
+}
+// The same mat-vec for K up to NXW_MAX (a wide layer 1): each slice's k in passes of KCM, in order.
+template <int NT>
+__device__ __forceinline__ float base_matvec_wide(const float* __restrict__ Wt, const float* v, int K, int H,
+                                               float (*part)[HMAX]) {
+  constexpr int KCM = HMAX * HMAX / 4 / NT;
+  const int tid = threadIdx.x;
+  const int G4 = H >> 2, g = tid % G4, sl = tid / G4, ns = NT / G4;
+  const int kc = (K + ns - 1) / ns, k0 = sl * kc;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb < kc; kb += KCM) {
     float4 w[KCM];
 #pragma unroll
-    for (int j = 0; j < KCM; ++j)  // all loads in flight
+    for (int j = 0; j < KCM; ++j)
       w[j] = (kb + j < kc && k0 + kb + j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)(k0 + kb + j) * H + 4 * g)
                                               : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -1333,7 +1366,6 @@ __device__ __forceinline__ float base_matvec(const float* __restrict__ Wt, const
         a[3] = fmaf(w[j].w, vk, a[3]);
       }
   }
-  // lanes g + G4 s of this wave hold the same units: sum them over the lane bits >= log2(G4)
   for (int o = G4; o < 64; o <<= 1)
 #pragma unroll
     for (int r = 0; r < 4; ++r) a[r] += __shfl_xor(a[r], o, 64);
@@ -1398,12 +1430,15 @@ __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, co
         if (d < nx) row[1 + d] = x[q];
         bs.xs[d] = d < nx ? x[q] : 0.f;
       }
+    } else if (4 * nb <= tid && tid < NXP_MAX) {
+      bs.xs[tid] = 0.f;
     }
-    for (int d = 4 * nb + tid; d < NXW_MAX; d += NT) bs.xs[d] = 0.f;
   } else {
     const float* row = tx + (size_t)i * F;
     if (tid == 0) bs.ts = row[0];
-    for (int d = tid; d < NXW_MAX; d += NT) bs.xs[d] = d < nx ? row[1 + d] : 0.f;
+    if (tid < NXP_MAX) bs.xs[tid] = tid < nx ? row[1 + tid] : 0.f;
+    if (nx > NXP_MAX)  // wide problems: the rest of x (only dims < nx are read)
+      for (int d = NXP_MAX + tid; d < nx; d += NT) bs.xs[d] = row[1 + d];
   }
   __syncthreads();
   const float t = bs.ts;
@@ -1443,7 +1478,8 @@ __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, co
   const int H = net.H, L = net.L, nxp = net.nxp;
   // layer 1
   {
-    const float acc = base_matvec<NT>(net.W1xT, bs.xs, nx, H, bs.part);
+    const float acc = nx <= NXP_MAX ? base_matvec<NT>(net.W1xT, bs.xs, nx, H, bs.part)
+                                    : base_matvec_wide<NT>(net.W1xT, bs.xs, nx, H, bs.part);
     if (tid < H) {
       const float v = net.b1[tid] + acc;
       bx[(size_t)i * H + tid] = v;
