@@ -22,7 +22,8 @@ UNITS = ["dpi_kernels.hip", "dpi_paths_cha.hip", "dpi_paths_ou.hip", "dpi_paths_
          "dpi_paths_td_ou.hip", "dpi_paths_td_gbm.hip", "dpi_paths_cha_tanh.hip", "dpi_paths_ou_tanh.hip",
          "dpi_paths_gbm_tanh.hip", "dpi_paths_td_cha_tanh.hip", "dpi_paths_td_ou_tanh.hip", "dpi_paths_td_gbm_tanh.hip",
          "dpi_paths_fb_cha.hip", "dpi_paths_fb_ou.hip", "dpi_paths_wide_cha.hip", "dpi_paths_wide_ou.hip",
-         "dpi_paths_wide_cha_tanh.hip", "dpi_paths_wide_ou_tanh.hip"]
+         "dpi_paths_wide_cha_tanh.hip", "dpi_paths_wide_ou_tanh.hip", "dpi_paths_wide_gbm.hip",
+         "dpi_paths_wide_gbm_tanh.hip"]
 OBJ = ROOT / "build"
 OUT = ROOT / "libdpi_hip.so"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

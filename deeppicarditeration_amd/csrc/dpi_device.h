@@ -67,6 +67,7 @@ constexpr int NXP_MAX = 128;       // max padded state dimension of the two-work
 // max state dimension of the wide first-order instances (Cha / OU, one workgroup per CU: the noise
 // tile of 256 dims x 64 paths is 70 KB of LDS; dpi_paths_wide_*.hip)
 constexpr int NXW_MAX = 256;
+constexpr int HBS = NXW_MAX;  // row stride of the GBM baseline Hessian diagonal in the workspace (hb[n][HBS])
 constexpr int HMAX = 128;
 
 struct NetDev {
@@ -724,41 +725,70 @@ __device__ __forceinline__ void mlp_tile_split(const EqDev& e, const NetDev& net
 }
 
 // LDS of the fully-nonlinear (GBM) path kernel: every weight matrix stays resident for the
-// 100-direction tangent sweep.  H <= 64, L <= 4.
-template <int H>
+// 100-direction tangent sweep.  H <= 64, L <= 4.  Wide instances (NXW = NXW_MAX, nx <= 256): the
+// 256-row noise tile leaves no room for W1x (it is read from L2: layer 0's A operand and the sweep's
+// z_0 = W1x[:, d] as a row of W1x^T) and the hidden weights are resident for L <= 3.
+template <int H, int NXW_ = NXP_MAX>
 struct LdsGbm {
-  static constexpr int NXW = NXP_MAX;
+  static constexpr int NXW = NXW_;
+  static constexpr bool W1X_LDS = NXW == NXP_MAX;
   static constexpr int WXS = NXP_MAX + 8;  // W1x row stride (WXS/4 = 2 mod 4)
   static constexpr int WHS = H + 8;        // hidden row stride
-  float S[NXP_MAX * SS];
-  float W1x[H * WXS];
-  float Wh[3][H * WHS];
+  static constexpr int NWH = W1X_LDS ? 3 : 2;
+  float S[NXW * SS];
+  float W1x[W1X_LDS ? H * WXS : 4];
+  float Wh[NWH][H * WHS];
   float vec[4 * HMAX];
   float bh[4 * HMAX];
-  float xsh[NXP_MAX];
-  float hb[NXP_MAX];
+  float xsh[NXW];
+  float hb[NXW];
   float gst[4 * P * NSG];
   float fst[4 * P * NSG];
   float wx[NSG];
   float tau[P], cmul[P], bsh[P], fbp[P];
   float smt[P];                    // Hessian labels: s - t per path
-  unsigned char cnt[NXP_MAX * P];  // SDGD index histogram [d][path]
+  unsigned char cnt[NXW * P];      // SDGD index histogram [d][path]
   // SDGD: each path's distinct sampled directions in increasing order (mlp_hdiag_split's sweep;
   // H >= 32 only — the u = 0 and H = 16 instances keep their LDS under 80 KB, two blocks per CU)
   static constexpr int DLCAP = H >= 32 ? 96 : 1;
   unsigned char dl[P * DLCAP];
 };
 
+// Row h of W1x from the GBM LDS image (stride WXS) or, in the wide instances, from L2 (stride nxp).
+template <int H, int NXW>
+__device__ __forceinline__ const float* gbm_w1x_row(const LdsGbm<H, NXW>& sh, const NetDev& net, int h) {
+  if constexpr (LdsGbm<H, NXW>::W1X_LDS)
+    return sh.W1x + h * LdsGbm<H, NXW>::WXS;
+  else
+    return net.W1x + (size_t)h * net.nxp;
+}
+// z_0 = W1x[:, d] for this lane's units 16 T + 4 qq + r (LDS column reads, or one 16-B row chunk of
+// W1x^T per T in the wide instances)
+template <int H, int NXW>
+__device__ __forceinline__ void gbm_w1x_col(const LdsGbm<H, NXW>& sh, const NetDev& net, int d, int qq,
+                                            float (&z)[H / 16][4]) {
+#pragma unroll
+  for (int T = 0; T < H / 16; ++T) {
+    if constexpr (LdsGbm<H, NXW>::W1X_LDS) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * LdsGbm<H, NXW>::WXS + d];
+    } else {
+      const float4 v = *reinterpret_cast<const float4*>(net.W1xT + (size_t)d * H + 16 * T + 4 * qq);
+      z[T][0] = v.x, z[T][1] = v.y, z[T][2] = v.z, z[T][3] = v.w;
+    }
+  }
+}
+
 // Diagonal of the x-Hessian of u at (s, X_s) for this wave's 16 paths, contracted with the
 // path's SDGD index histogram: s1 = sum_d cnt[d] u_dd, s2 = sum_d cnt[d] |u_dd|.
 // Uses u_dd = sum_l < lam_l, elu''(z_l) * zdot_l^2 >, with lam_l = du/da_l (one backward pass)
 // and zdot_l = dz_l/dx_d (first-order tangents only): half the MACs of second-order
 // forward mode.  All GEMMs are v_mfma_f32_16x16x4_f32 in the hidden x path orientation.
-template <int H, int L, int ACT>
-__device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt, float& s1_out,
+template <int H, int L, int ACT, int NXW>
+__device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, LdsGbm<H, NXW>& sh, int nxt, float& s1_out,
                                           float& s2_out) {
   constexpr int HT = H / 16;
-  constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+  constexpr int WHS = LdsGbm<H, NXW>::WHS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int jj = lane & 15, qq = lane >> 4;
   const int pp = 16 * wv + jj;
@@ -770,7 +800,7 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
 #pragma unroll
   for (int T = 0; T < HT; ++T) {
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    const float* wrow = gbm_w1x_row(sh, net, 16 * T + jj) + 4 * qq;
     for (int t = 0; t < nxt; ++t) {
       const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
       const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
@@ -832,13 +862,11 @@ __device__ __forceinline__ void mlp_hdiag(const EqDev& e, const NetDev& net, Lds
   for (int d = 0; d < e.nx; ++d) {
     float z[HT][4];
     float term = 0.f;
+    gbm_w1x_col(sh, net, d, qq, z);
 #pragma unroll
     for (int T = 0; T < HT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        z[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
-        term = fmaf(lam[0][T][r] * Act<ACT>::d2(act[0][T][r]), z[T][r] * z[T][r], term);
-      }
+      for (int r = 0; r < 4; ++r) term = fmaf(lam[0][T][r] * Act<ACT>::d2(act[0][T][r]), z[T][r] * z[T][r], term);
 #pragma unroll
     for (int l = 1; l < L; ++l) {
       float Bm[HT][4];
@@ -897,12 +925,11 @@ __device__ __forceinline__ void split8u(const float (&x)[8], half8& hi, half8& l
     lo[j] = l.x, lo[j + 1] = l.y;
   }
 }
-template <int H, int L, int ACT>
-__device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H>& sh, int nxt,
+template <int H, int L, int ACT, int NXW>
+__device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& net, LdsGbm<H, NXW>& sh, int nxt,
                                                 float& s1_out, float& s2_out) {
   static_assert(H % 32 == 0, "split hdiag needs H % 32 == 0");
   constexpr int HT = H / 16, NU = H / 32, LH = L > 1 ? L - 1 : 1;
-  constexpr int WXS = LdsGbm<H>::WXS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int jj = lane & 15, qq = lane >> 4;
   const int pp = 16 * wv + jj;
@@ -965,7 +992,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 #pragma unroll
   for (int T = 0; T < HT; ++T) {
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    const float* wrow = gbm_w1x_row(sh, net, 16 * T + jj) + 4 * qq;
     for (int t = 0; t < nxt; ++t) {
       const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
       const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
@@ -1052,12 +1079,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
   float s1 = 0.f, s2 = 0.f;
   // z_0 = W1x[:, d] of the next direction is read from LDS while this direction's MFMAs run: two
   // register sets, the direction loop unrolled by 2 so they swap roles without copies
-  auto ldz = [&](int d, float (&zz)[HT][4]) {
-#pragma unroll
-    for (int T = 0; T < HT; ++T)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) zz[T][r] = sh.W1x[(16 * T + 4 * qq + r) * WXS + d];
-  };
+  auto ldz = [&](int d, float (&zz)[HT][4]) { gbm_w1x_col(sh, net, d, qq, zz); };
   // one direction: z (in) is clobbered; zn receives z_0 of direction dn; counted: weight cnt (else 0)
   auto direction = [&](int d, float (&z)[HT][4], float (&zn)[HT][4], int dn, bool counted) {
     f32x2 term2 = {0.f, 0.f};
@@ -1101,17 +1123,22 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
   int ndp = e.nx, kmax = e.nx;
   bool lists = false;
   if (e.sdgd_v > 0) {
-    constexpr int DLCAP = LdsGbm<H>::DLCAP;
+    constexpr int DLCAP = LdsGbm<H, NXW>::DLCAP;
     // the path's four lanes build its list together: lane qq scans dims [qq dq, (qq + 1) dq) (all
     // its histogram bytes read at once), places its sampled dims after the lower quarters' counts
     // (a prefix over the path's lanes jj + 16 q), so the list is in increasing order
-    constexpr int QD = NXP_MAX / 4;
+    constexpr int QD = NXW / 4;
+    using MaskT = std::conditional_t<(QD > 32), unsigned long long, uint32_t>;
     const int dq = (e.nx + 3) >> 2, d0 = qq * dq;
-    uint32_t mq = 0;
+    MaskT mq = 0;
 #pragma unroll
     for (int i = 0; i < QD; ++i)
-      if (i < dq && d0 + i < e.nx && sh.cnt[(d0 + i) * P + pp]) mq |= 1u << i;
-    const int cq = __popc(mq);
+      if (i < dq && d0 + i < e.nx && sh.cnt[(d0 + i) * P + pp]) mq |= (MaskT)1 << i;
+    int cq;
+    if constexpr (QD > 32)
+      cq = __popcll(mq);
+    else
+      cq = __popc(mq);
     int base = 0;
     ndp = 0;
 #pragma unroll
@@ -1121,7 +1148,11 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
       ndp += v;
     }
     for (int k = base; mq; ++k) {
-      const int b = __builtin_ctz(mq);
+      int b;
+      if constexpr (QD > 32)
+        b = __builtin_ctzll(mq);
+      else
+        b = __builtin_ctz(mq);
       mq &= mq - 1;
       if (k < DLCAP) sh.dl[pp * DLCAP + k] = (unsigned char)(d0 + b);
     }
@@ -1134,7 +1165,7 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
     lists = kmax <= DLCAP;
   }
   if (lists) {
-    constexpr int DLCAP = LdsGbm<H>::DLCAP;
+    constexpr int DLCAP = LdsGbm<H, NXW>::DLCAP;
     auto dir = [&](int k) { return (int)sh.dl[pp * DLCAP + min(k, ndp - 1)]; };
     int k = 0, dk = dir(0);
     ldz(dk, za);
@@ -1160,10 +1191,10 @@ __device__ __forceinline__ void mlp_hdiag_split(const EqDev& e, const NetDev& ne
 
 // u(tau, x + cmul S) for this wave's 16 paths with every weight LDS-resident (GBM layout):
 // the forward half of mlp_hdiag.  The TD terminal value (data.py:941-942).
-template <int H, int L, int ACT>
-__device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh, int nxt) {
+template <int H, int L, int ACT, int NXW>
+__device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H, NXW>& sh, int nxt) {
   constexpr int HT = H / 16;
-  constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
+  constexpr int WHS = LdsGbm<H>::WHS;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int jj = lane & 15, qq = lane >> 4;
   const int pp = 16 * wv + jj;
@@ -1173,7 +1204,7 @@ __device__ __forceinline__ float mlp_value_res(const NetDev& net, LdsGbm<H>& sh,
 #pragma unroll
   for (int T = 0; T < HT; ++T) {
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = sh.W1x + (16 * T + jj) * WXS + 4 * qq;
+    const float* wrow = gbm_w1x_row(sh, net, 16 * T + jj) + 4 * qq;
     for (int t = 0; t < nxt; ++t) {
       const float4 a = *reinterpret_cast<const float4*>(wrow + 16 * t);
       const float* bc = sh.S + (16 * t + 4 * qq) * SS + pp;
@@ -1537,13 +1568,14 @@ __global__ __launch_bounds__(NTB) void k_baseline(EqDev e, NetDev net, const flo
 // GBM per-point baseline (one 1024-thread workgroup per point): g(x), the exact-solution part of
 // ffi at (t, x) (equations.py:457-466), bx = b1 + W1[:,1:] x and the network's Hessian diagonal at
 // (t, x) for the SDGD baseline gather (data.py:1293-1302).  smp / tickets as base_point.
-template <bool ZERO>
+// NXW = NXW_MAX: the wide instance (nx <= 256), whose tangent sweep runs once per 128 columns.
+template <bool ZERO, int NXW = NXP_MAX>
 __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, const float* __restrict__ tx, int n,
                                                       float* __restrict__ gx, float* __restrict__ fb,
                                                       float* __restrict__ bx, float* __restrict__ hb, SampleSpec smp,
                                                       int* __restrict__ tickets) {
   constexpr int KIND = DPI_EQ_GBM;
-  __shared__ float xs[NXP_MAX];
+  __shared__ float xs[NXW];
   __shared__ float act[4][HMAX];
   __shared__ float red[NTHB / 64];
   __shared__ float ts;
@@ -1569,13 +1601,13 @@ __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, cons
         if (d < nx) row[1 + d] = x[q];
         xs[d] = d < nx ? x[q] : 0.f;
       }
-    } else if (4 * nb <= tid && tid < NXP_MAX) {
+    } else if (4 * nb <= tid && tid < NXW) {
       xs[tid] = 0.f;
     }
   } else {
     const float* row = tx + (size_t)i * F;
     if (tid == 0) ts = row[0];
-    for (int d = tid; d < NXP_MAX; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
+    for (int d = tid; d < NXW; d += NTHB) xs[d] = d < nx ? row[1 + d] : 0.f;
   }
   __syncthreads();
   const float t = ts;
@@ -1631,7 +1663,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, cons
   const float ah = block_sum_n<NTHB>(Eq<KIND>::abs_hess_partial(e, sn, tid, NTHB), red);
   const float Cb = Eq<KIND>::exact_scalar_terms(e, arg) - 0.25f * ah;
   if (ZERO) {
-    for (int d = tid; d < NXP_MAX; d += NTHB) hb[(size_t)i * NXP_MAX + d] = 0.f;
+    for (int d = tid; d < NXW; d += NTHB) hb[(size_t)i * HBS + d] = 0.f;
     if (tid == 0) fb[i] = Cb;
     return;
   }
@@ -1678,6 +1710,10 @@ __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, cons
   __shared__ float udp[16][NXP_MAX];
   const bool sw = tid < 512;
   const int dg = tid & 31, hg = (tid >> 5) & 15, RJ = (H + 15) >> 4;
+  // columns c0 .. c0 + 127 of the diagonal per pass (one pass for NXW = 128)
+#pragma unroll 1
+  for (int c0 = 0; c0 < NXW; c0 += NXP_MAX) {
+  if (NXW > NXP_MAX && c0 >= nx) break;
   float ud[4] = {0.f, 0.f, 0.f, 0.f};
   if (sw) {
 #pragma unroll
@@ -1687,7 +1723,7 @@ __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, cons
         float z[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int d = 4 * dg + q;
+          const int d = c0 + 4 * dg + q;
           z[q] = d < nx ? net.W1x[(size_t)h * nxp + d] : 0.f;
         }
         *reinterpret_cast<float4*>(&ztb[0][h][4 * dg]) = make_float4(z[0], z[1], z[2], z[3]);
@@ -1756,7 +1792,9 @@ __global__ __launch_bounds__(NTHB) void k_baseline_gbm(EqDev e, NetDev net, cons
   if (tid < NXP_MAX) {
     float a = 0.f;
     for (int g = 0; g < 16; ++g) a += udp[g][tid];
-    hb[(size_t)i * NXP_MAX + tid] = tid < nx ? a : 0.f;
+    hb[(size_t)i * HBS + c0 + tid] = c0 + tid < nx ? a : 0.f;
+  }
+  if (NXW > NXP_MAX) __syncthreads();  // udp and ztb are reused by the next pass
   }
   if (tid == 0) fb[i] = Cb;
 }
@@ -1766,7 +1804,7 @@ struct PathArgs {
   const float* gx;
   const float* fb;
   const float* bx;
-  const float* hb;  // GBM: baseline Hessian diagonal [n][NXP_MAX]
+  const float* hb;  // GBM: baseline Hessian diagonal [n][HBS]
   float* partial;
   int n, nbp, m_begin, K, flags;
   uint32_t k0, k1, c3t, c3s, c3i, c3q, point_base;
@@ -2196,9 +2234,10 @@ template <int KIND, int H, int L, bool ZERO, bool SPLIT, bool HESS, bool TD, int
 __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, const PathArgs& a, const FusedBase& fb) {
   static_assert(!HESS || KIND == DPI_EQ_GBM, "Hessian labels: GBM (SimpleDiffusionEquationWithHessian) only");
   static_assert(!(HESS && TD), "the Hessian-label estimators have no TD variant (data.py:1220-1223)");
-  static_assert(NXW == NXP_MAX || (KIND != DPI_EQ_GBM && !HESS && !FBT && NXW % 128 == 0 && NXW <= NXW_MAX),
-                "wide instances: first-order Cha / OU labels, no fused baseline");
-  using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H>, LdsT<NXW>>;
+  static_assert(NXW == NXP_MAX || (!HESS && !TD && !FBT && NXW % 128 == 0 && NXW <= NXW_MAX),
+                "wide instances: first-order labels, no TD, no fused baseline");
+  static_assert(!(KIND == DPI_EQ_GBM && NXW > NXP_MAX) || L <= 3, "wide GBM instances: the hidden weights of L <= 3");
+  using SH = std::conditional_t<KIND == DPI_EQ_GBM, LdsGbm<H, NXW>, LdsT<NXW>>;
   constexpr int NBW = NXW / 16;  // dim-blocks of 4 per wave (4 waves)
   __shared__ SH sh;
   constexpr bool GBM = KIND == DPI_EQ_GBM;
@@ -2281,19 +2320,21 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
       for (int h = tid; h < H; h += NTH) sh.bh[l * H + h] = net.b[l][h];
   }
   if constexpr (GBM) {
-    if (!ZERO) {  // all weights resident for the tangent sweep
-      constexpr int WXS = LdsGbm<H>::WXS, WHS = LdsGbm<H>::WHS;
-      for (int idx = tid; idx < H * nxp; idx += NTH) {
-        const int h = idx / nxp, d = idx - h * nxp;
-        sh.W1x[h * WXS + d] = net.W1x[idx];
-      }
+    if (!ZERO) {  // all weights resident for the tangent sweep (wide instances: W1x from L2)
+      [[maybe_unused]] constexpr int WXS = SH::WXS;
+      constexpr int WHS = SH::WHS;
+      if constexpr (SH::W1X_LDS)
+        for (int idx = tid; idx < H * nxp; idx += NTH) {
+          const int h = idx / nxp, d = idx - h * nxp;
+          sh.W1x[h * WXS + d] = net.W1x[idx];
+        }
       for (int l = 1; l < L; ++l)
         for (int idx = tid; idx < H * H; idx += NTH) {
           const int h = idx / H, k = idx - h * H;
           sh.Wh[l - 1][h * WHS + k] = net.W[l][idx];
         }
     }
-    for (int d = tid; d < nxp; d += NTH) sh.hb[d] = d < nx ? a.hb[(size_t)i * NXP_MAX + d] : 0.f;
+    for (int d = tid; d < nxp; d += NTH) sh.hb[d] = d < nx ? a.hb[(size_t)i * HBS + d] : 0.f;
     for (int idx = tid; idx < nxp * P / 4; idx += NTH) reinterpret_cast<uint32_t*>(sh.cnt)[idx] = 0u;
     if (wv == 0) {  // w_k . x for this point
 #pragma unroll
@@ -2682,7 +2723,12 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
         }
       }
       if (g0 == 0 && wv == 0) {
-        const float c0 = ap + bp + (INTG ? (f_b + Eq<KIND>::ffc(e)) * tmt : 0.f);
+        float fbt;
+        if constexpr (GBM)
+          fbt = sh.fbp[lane];
+        else
+          fbt = f_b + Eq<KIND>::ffc(e);
+        const float c0 = ap + bp + (INTG ? fbt * tmt : 0.f);
         col[56] = c0;
         col[57] = c0 * c0;
       }

@@ -73,7 +73,7 @@ constexpr bool fused_base_shape() {
 template <int KIND, int H, int L, bool Z, bool TDV, int ACT = DPI_ACT_ELU, bool FBV = false, int NXW = NXP_MAX>
 void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
   if constexpr (NXW > NXP_MAX) {
-    static_assert(KIND != DPI_EQ_GBM && !TDV && !FBV, "wide instances: first-order Cha / OU");
+    static_assert(!TDV && !FBV, "wide instances: first-order labels");
     if constexpr (!Z && H % 32 == 0) {
       if (q.a->split) {
         DPI_PATH_LAUNCH((k_paths<KIND, H, L, Z, true, false, false, ACT, NXW>), q, p->e, net->d, *q.a);
@@ -97,9 +97,14 @@ void do_launch(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q) {
                          net->d, *q.a);
     }
   } else if (q.baseline) {
-    if constexpr (KIND == DPI_EQ_GBM)
-      hipLaunchKernelGGL((k_baseline_gbm<Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
-                         q.bx, q.hb, q.smp, q.tickets);
+    if constexpr (KIND == DPI_EQ_GBM) {
+      if (p->e.nx > NXP_MAX)  // the wide baseline (nx <= 256)
+        hipLaunchKernelGGL((k_baseline_gbm<Z, NXW_MAX>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx,
+                           q.fb, q.bx, q.hb, q.smp, q.tickets);
+      else
+        hipLaunchKernelGGL((k_baseline_gbm<Z>), dim3(q.n), dim3(NTHB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
+                           q.bx, q.hb, q.smp, q.tickets);
+    }
     else
       hipLaunchKernelGGL((k_baseline<KIND, Z>), dim3(q.n), dim3(NTB), 0, q.st, p->e, net->d, q.tx, q.n, q.gx, q.fb,
                          q.bx, q.smp, q.tickets);
@@ -195,3 +200,5 @@ bool dispatch_wide_cha(const dpi_problem_s* p, const dpi_net_s* net, const Launc
 bool dispatch_wide_ou(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_wide_cha_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
 bool dispatch_wide_ou_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_gbm(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);
+bool dispatch_wide_gbm_tanh(const dpi_problem_s* p, const dpi_net_s* net, const Launch& q);

@@ -596,9 +596,9 @@ int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double m
 
 int dpi_problem_create_gbm(int nx, double alpha, double T, int n_nodes, const double* w, const double* v,
                            dpi_problem* out) {
-  if (nx > NXP_MAX) return fail(DPI_ERR_UNSUPPORTED, "gbm: nx exceeds the compiled maximum state dimension 128 (NXP_MAX)");
+  if (nx > NXW_MAX) return fail(DPI_ERR_UNSUPPORTED, "gbm: nx exceeds the compiled maximum state dimension 256 (NXW_MAX)");
   if (!out || nx < 1 || n_nodes < 1 || n_nodes > NSG || !w || !v)
-    return fail(DPI_ERR_ARG, "gbm: bad arguments (1 <= n_nodes <= 8, nx <= 128)");
+    return fail(DPI_ERR_ARG, "gbm: bad arguments (1 <= n_nodes <= 8, nx <= 256)");
   auto* p = new_problem(DPI_EQ_GBM, nx, alpha, T);
   p->e.nodes = n_nodes;
   const int F = 1 + nx;
@@ -1217,7 +1217,7 @@ static int pis_chunk_wg() {
   return v;
 }
 
-// Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][128] | tickets[n] | rec[n][BREC] | ready[n] |
+// Workspace: gx[n] | fb[n] | bx[n][H] | hb[n][HBS = 256] | tickets[n] | rec[n][BREC] | ready[n] |
 // [PIS rows] | partial[n][nbp][slab_row] | ...  (256-B aligned)
 struct WsLayout {
   size_t gx, fb, bx, hb, tk, rec, ready, rows, partial, rq, noise, nq, total;
@@ -1242,7 +1242,7 @@ static WsLayout ws_layout(dpi_net net, int n, int M, int F, bool noise = false) 
   w.fb = al256((size_t)n * 4);
   w.bx = w.fb + al256((size_t)n * 4);
   w.hb = w.bx + al256((size_t)n * H * 4);
-  w.tk = w.hb + al256((size_t)n * NXP_MAX * 4);  // the fused reduce's per-point tickets (k_paths)
+  w.tk = w.hb + al256((size_t)n * HBS * 4);  // the fused reduce's per-point tickets (k_paths)
   // the one-launch dpi_sample_with_gradients' per-point baseline records and hand-off words
   w.rec = w.tk + al256((size_t)n * 4);
   w.ready = w.rec + al256((size_t)n * BREC * 4);
@@ -1591,6 +1591,8 @@ static bool dispatch_any(const dpi_problem_s* p, const dpi_net_s* net, const Lau
         return tanh ? dispatch_wide_cha_tanh(p, net, q) : dispatch_wide_cha(p, net, q);
       case DPI_EQ_OU:
         return tanh ? dispatch_wide_ou_tanh(p, net, q) : dispatch_wide_ou(p, net, q);
+      case DPI_EQ_GBM:
+        return tanh ? dispatch_wide_gbm_tanh(p, net, q) : dispatch_wide_gbm(p, net, q);
       default:
         return false;
     }
@@ -2264,6 +2266,8 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.hpart = (float*)(b + base);
   const int NT = (nx + 15) / 16;
   hipStream_t st = (hipStream_t)stream;
+  if (p->e.nx > NXP_MAX)
+    return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: compiled for nx <= 128 (NXP_MAX)");
   Launch q{false, nullptr, 0, nullptr, nullptr, nullptr, nullptr, &a, n * nbp, st};
   q.hess = true;
   take_timer(q.t0, q.t1);
