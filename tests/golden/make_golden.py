@@ -348,6 +348,12 @@ def main(only=None):
              85, workdir=wd)
     run_case("wide_ou256_mlp128x4_K2", "OUProcessEquation", {**ou, "nx": 256}, "mlp", {"neurons": [128] * 4}, 2, 64,
              2, 86, workdir=wd)
+    run_case("wide_gbm200_mlp64x3_sdgd_K2", "GBMEquationComplexExact", {**gbm, "nx": 200}, "mlp", {"neurons": [64] * 3},
+             2, 64, 2, 87, v=100, workdir=wd)
+    run_case("wide_gbm256_mlp32x2_tanh_sdgd_K2", "GBMEquationComplexExact", {**gbm, "nx": 256}, "mlp",
+             {"neurons": [32, 32], "act": "Tanh"}, 2, 64, 2, 88, v=200, workdir=wd)
+    run_case("wide_gbm256_mlp16_full_K1", "GBMEquationComplexExact", {**gbm, "nx": 256}, "mlp", {"neurons": [16, 16]},
+             2, 64, 1, 89, workdir=wd)
     shutil.rmtree(wd)
 
 

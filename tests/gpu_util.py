@@ -21,7 +21,9 @@ def product_equation(f):
         assert np.allclose(e.mean.numpy(), f["gmm_mean"]) and np.allclose(e.pi.numpy(), f["gmm_pi"])
         return e
     if eq == "GBMEquationComplexExact":
-        return dpi.GBMEquationComplexExact(int(f["eqkw_nx"]), float(f["eqkw_alpha"]), float(f["eqkw_T"]))
+        # the reference ships w / v for nx = 100 only; at other nx it drew them (equations.py:408-420)
+        wv = {} if int(f["eqkw_nx"]) == 100 else dict(w=f["gbm_w"], v=f["gbm_v"])
+        return dpi.GBMEquationComplexExact(int(f["eqkw_nx"]), float(f["eqkw_alpha"]), float(f["eqkw_T"]), **wv)
     raise ValueError(eq)
 
 

@@ -45,16 +45,17 @@ def test_host_side_argument_errors_without_gpu():
     assert lib.dpi_problem_create_cha(0, 1.0, 5.0, 1.0, h) == _lib.DPI_ERR_ARG
     assert "cha" in _lib.last_error()
     # the compiled state-dimension caps are named refusals (include/dpi.h): 256 for
-    # Cha / OU and MLP nets (the wide first-order instances), 128 for GBM and PISGradNet
+    # the problems and MLP nets (the wide first-order instances), 128 for PISGradNet, the Hessian
+    # labels and the TD estimators (tests/test_gpu_wide.py)
     assert lib.dpi_problem_create_cha(257, 1.0, 5.0, 1.0, h) == _lib.DPI_ERR_UNSUPPORTED
     assert "256" in _lib.last_error()
     assert lib.dpi_net_create_mlp(258, 2, (ctypes.c_int * 2)(16, 16), _lib.DPI_ACT_ELU,
                                   (ctypes.c_float * 1)(), 1, ctypes.byref(ctypes.c_void_p())) == _lib.DPI_ERR_UNSUPPORTED
     assert "256" in _lib.last_error()
-    w = (ctypes.c_double * (2 * 201))()
+    w = (ctypes.c_double * (2 * 258))()
     v = (ctypes.c_double * 2)(1.0, 1.0)
-    assert lib.dpi_problem_create_gbm(200, 1.0, 1.0, 2, w, v, h) == _lib.DPI_ERR_UNSUPPORTED
-    assert "128" in _lib.last_error()
+    assert lib.dpi_problem_create_gbm(257, 1.0, 1.0, 2, w, v, h) == _lib.DPI_ERR_UNSUPPORTED
+    assert "256" in _lib.last_error()
     # activations: ELU and Tanh only
     assert lib.dpi_net_create_mlp(101, 2, (ctypes.c_int * 2)(16, 16), 3, (ctypes.c_float * 1)(), 1,
                                   ctypes.byref(ctypes.c_void_p())) == _lib.DPI_ERR_UNSUPPORTED

@@ -1,8 +1,8 @@
-"""State dimensions above 128: the wide first-order instances (Cha / OU, nx <= NXW_MAX = 256,
+"""State dimensions above 128: the wide first-order instances (Cha / OU / GBM, nx <= NXW_MAX = 256,
 one workgroup per CU) against the reference's own labels (tests/golden/wide_*,
 made by tests/golden/make_golden.py from picard/data.py at nx = 200 and 256) and against the fp64
-oracle, in both MFMA modes; and the refusals that remain (TD estimators, GBM, PISGradNet above 128).
-Reference: every equation takes any nx (picard/equations.py:266-338, 599-714)."""
+oracle, in both MFMA modes; and the refusals that remain (TD estimators, Hessian labels, PISGradNet
+above 128).  Reference: every equation takes any nx (picard/equations.py:266-338, 388-486, 599-714)."""
 import numpy as np
 import pytest
 import torch
@@ -39,7 +39,7 @@ def precision(request):
 def test_wide_fixtures_cover_200_and_256():
     nxs = {int(load(c)["eqkw_nx"]) for c in WIDE}
     eqs = {str(load(c)["eq"]) for c in WIDE}
-    assert {200, 256} <= nxs and {"Cha", "OUProcessEquation"} <= eqs
+    assert {200, 256} <= nxs and {"Cha", "OUProcessEquation", "GBMEquationComplexExact"} <= eqs
 
 
 @pytest.mark.parametrize("case", WIDE)
@@ -126,6 +126,51 @@ def test_wide_ou_gmm_vs_oracle(precision):
     assert parts["value"] < TOL and parts["grad"] < TOL, parts
 
 
+@pytest.mark.parametrize("v", [100, 0])
+def test_wide_gbm_config5_network_vs_oracle(v, precision):
+    """The configs[4] network (3 x 64 ELU) at nx = 240, K = 20: SDGD v = 100 (the per-path direction
+    lists, 64-bit list masks) and the exact diagonal (v = 0: all 240 directions), against the oracle."""
+    import deeppicarditeration_amd as dpi
+    rng = np.random.default_rng(5)
+    nx = 240
+    w = rng.standard_normal((2, 1 + nx)) / np.sqrt(nx)
+    w[:, 0] = 1.0
+    vv = rng.standard_normal((2, 1))
+    eq = dpi.GBMEquationComplexExact(nx, 1.0, 1.0, w=w, v=vv)
+    net = _mlp(eq, [64] * 3, 6)
+    hess = {"method": "SDGD", "kwargs": {"v": v}} if v else None
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=128,
+                                  n_estimate_integral=128, n_euler_steps=20, seed=3, epoch=2, hessian_approximation=hess)
+    tx, y = gen.sample_with_gradients(2)
+    oeq = O.GBMEquationComplexExact(nx, eq.w.numpy(), eq.v.numpy())
+    ref = O.labels_grad(oeq, _oracle_mlp(net), tx.cpu().double().numpy(), 128, 20, 3, 2, 0, v=v)
+    parts = rel_l2_parts(y.cpu().numpy(), ref)
+    print("gbm wide", v, precision, parts)
+    assert parts["value"] < TOL and parts["grad"] < TOL, parts
+
+
+def test_wide_gbm_prepared_equals_plain():
+    """The GBM prepare schedule (noise sums staged by k_noise_shared on the side stream) at nx = 200:
+    bitwise the unprepared labels."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+    rng = np.random.default_rng(8)
+    nx = 200
+    w = rng.standard_normal((2, 1 + nx)) / np.sqrt(nx)
+    w[:, 0] = 1.0
+    eq = dpi.GBMEquationComplexExact(nx, 1.0, 1.0, w=w, v=rng.standard_normal((2, 1)))
+    net = _mlp(eq, [64] * 3, 9)
+    gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=1024,
+                                  n_estimate_integral=1024, n_euler_steps=5, seed=4,
+                                  hessian_approximation={"method": "SDGD", "kwargs": {"v": 100}})
+    lab = ShardedLabeler(gen, rank=0, world=1)
+    prep = lab.prepare(8)
+    tx, pb = prep[:2]
+    y_prep = lab.end(lab.begin(prepared=prep))
+    y_plain = ShardedLabeler(gen, rank=0, world=1).labels(tx, pb)
+    assert torch.equal(y_prep, y_plain)
+
+
 def test_wide_labels_are_shard_invariant():
     """4,096 paths as 2 and 4 MC shards reduce to the one-call moments bit for bit (M / 64 G a power
     of two), as on 2 / 4 GPUs; the labels are bitwise reproducible."""
@@ -150,7 +195,8 @@ def test_wide_labels_are_shard_invariant():
 
 
 def test_wide_refusals_name_the_cap():
-    """What stays at nx <= 128: the TD estimators, GBM and PISGradNet (named refusals)."""
+    """What stays at nx <= 128: the TD estimators, the Malliavin Hessian labels and PISGradNet (named
+    refusals)."""
     import deeppicarditeration_amd as dpi
     from deeppicarditeration_amd._lib import DPIError
     eq = dpi.Cha(200, 1.0, 5.0, 1.0)
@@ -159,5 +205,14 @@ def test_wide_refusals_name_the_cap():
                                   n_estimate_integral=64, n_euler_steps=2, seed=1, estimate_delta_t=0.3)
     with pytest.raises((DPIError, NotImplementedError), match="128"):
         gen.sample_with_gradients(2)
-    with pytest.raises((DPIError, NotImplementedError, ValueError), match="128"):
-        dpi.GBMEquationComplexExact(200, 1.0, 1.0, w=np.full((2, 201), 0.1), v=np.ones(2)).dpi_problem()
+    g = dpi.GBMEquationComplexExact(200, 1.0, 1.0, w=np.full((2, 201), 0.1), v=np.ones((2, 1)))
+    gen = dpi.OnlineDataGenerator(g, _mlp(g, [32, 32], 2), 1, 1, device="cuda:0", t_always_uniform=True,
+                                  n_estimate_terminal=64, n_estimate_integral=64, n_euler_steps=2, seed=1)
+    with pytest.raises((DPIError, NotImplementedError), match="128"):
+        gen.sample_with_gradients_and_hessians(2)
+    o = dpi.OUProcessEquation(nx=200, T=1.0, alpha=1.0, num_components=2, mean=np.zeros((2, 200)),
+                              var=np.full((2, 200), 2.0), pi=np.full(2, 0.5))
+    pis = dpi.PISGradNet(hidden_shapes=[32, 32], dim=200, g0=o.g, T=1.0)
+    with pytest.raises((DPIError, NotImplementedError), match="128"):
+        dpi.OnlineDataGenerator(o, pis, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=64,
+                                n_estimate_integral=64, n_euler_steps=2, seed=1).sample_with_gradients(2)
