@@ -1432,7 +1432,9 @@ constexpr int BREC = 32 + HMAX;
 // coalesced through the transposed copies).  smp.tx != null: the block first samples its point
 // (draws 1-3, k_sample_points' arithmetic) into smp.tx and its LDS copy; tickets != null: zero the
 // point's ticket of the fused label reduce; rec != null: the values also go to the point's record.
-template <int KIND, bool ZERO, int NT>
+// WIDE: also nx > 128 (k_baseline; the fused launch's base blocks serve nx <= 128 only and keep
+// round 5's code)
+template <int KIND, bool ZERO, int NT, bool WIDE = true>
 __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, const float* __restrict__ tx, int i,
                                            float* __restrict__ gx, float* __restrict__ fb, float* __restrict__ bx,
                                            float* __restrict__ rec, const SampleSpec& smp, int* __restrict__ tickets,
@@ -1468,7 +1470,7 @@ __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, co
     const float* row = tx + (size_t)i * F;
     if (tid == 0) bs.ts = row[0];
     if (tid < NXP_MAX) bs.xs[tid] = tid < nx ? row[1 + tid] : 0.f;
-    if (nx > NXP_MAX)  // wide problems: the rest of x (only dims < nx are read)
+    if (WIDE && nx > NXP_MAX)  // wide problems: the rest of x (only dims < nx are read)
       for (int d = NXP_MAX + tid; d < nx; d += NT) bs.xs[d] = row[1 + d];
   }
   __syncthreads();
@@ -1509,8 +1511,8 @@ __device__ __forceinline__ void base_point(const EqDev& e, const NetDev& net, co
   const int H = net.H, L = net.L, nxp = net.nxp;
   // layer 1
   {
-    const float acc = nx <= NXP_MAX ? base_matvec<NT>(net.W1xT, bs.xs, nx, H, bs.part)
-                                    : base_matvec_wide<NT>(net.W1xT, bs.xs, nx, H, bs.part);
+    const float acc = (!WIDE || nx <= NXP_MAX) ? base_matvec<NT>(net.W1xT, bs.xs, nx, H, bs.part)
+                                               : base_matvec_wide<NT>(net.W1xT, bs.xs, nx, H, bs.part);
     if (tid < H) {
       const float v = net.b1[tid] + acc;
       bx[(size_t)i * H + tid] = v;
@@ -2248,7 +2250,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   if constexpr (FBC) {
     static_assert(sizeof(BaseLds<NTH>) <= sizeof(SH), "base blocks overlay the path LDS");
     if ((int)blockIdx.x < fb.nbase) {
-      base_point<KIND, ZERO, NTH>(e, net, a.tx, blockIdx.x, const_cast<float*>(a.gx), const_cast<float*>(a.fb),
+      base_point<KIND, ZERO, NTH, false>(e, net, a.tx, blockIdx.x, const_cast<float*>(a.gx), const_cast<float*>(a.fb),
                                   const_cast<float*>(a.bx), fb.rec, fb.smp, a.tickets,
                                   *reinterpret_cast<BaseLds<NTH>*>(&sh));
       base_publish(fb, blockIdx.x);

@@ -91,11 +91,11 @@ int dpi_abi_version(void);
 int dpi_last_error(char* buf, size_t len);
 
 /* --- problem plugins (host parameters copied to device; fp64 in, fp32 on device) ---
- * State dimensions: Cha and OU take nx <= 256 (NXW_MAX) with MLP and zero networks — above 128 the
- * first-order labels run on the wide path instances (one workgroup per CU); GBM, the
- * Hessian labels, the TD estimators and PISGradNet are compiled for nx <= 128 (NXP_MAX: the LDS-resident
- * GBM weights, k_pis_net's X image).  Past a cap a call fails with DPI_ERR_UNSUPPORTED naming it (the
- * reference's shipped configurations are 10-d and 100-d). */
+ * State dimensions: every problem takes nx <= 256 (NXW_MAX); above 128 the first-order labels of MLP
+ * and zero networks run on the wide path instances (one workgroup per CU).  The
+ * Malliavin Hessian labels, the TD estimators and PISGradNet are compiled for nx <= 128 (NXP_MAX).
+ * Past a cap a call fails with DPI_ERR_UNSUPPORTED naming it (the reference's shipped configurations
+ * are 10-d and 100-d). */
 int dpi_problem_create_cha(int nx, double alpha, double k, double T, dpi_problem* out);
 /* mean: (n_comp, nx); var_diag: (n_comp, nx) diagonal of each component covariance; pi: (n_comp) */
 int dpi_problem_create_ou(int nx, double alpha, double T, double theta, double mu, double alpha_scale,
