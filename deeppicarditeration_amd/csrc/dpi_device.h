@@ -2305,8 +2305,9 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   } else {
     for (int d = tid; d < nxp; d += NTH) sh.xsh[d] = d < nx ? txr[1 + d] : 0.f;
   }
-  // the split MLP reads the tile's first nxp32 rows (32-row chunks, 96 padded to 128)
-  const int nxpz = ZERO ? ((nxp + 31) & ~31) : max((nxp + 31) & ~31, net.nxp32);
+  // the split MLP reads the tile's first nxp32 rows (32-row chunks; the host pads nxp with it when
+  // it rounds a 96-word chunk up to 128, so this bound covers them)
+  const int nxpz = (nxp + 31) & ~31;
   for (int idx = tid; idx < (nxpz - 4 * nb) * P; idx += NTH) {  // zero pad rows of the noise tile
     const int d = 4 * nb + idx / P, p = idx % P;
     sh.S[d * SS + p] = 0.f;

@@ -734,7 +734,14 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   if (n_params != expect) return fail(DPI_ERR_ARG, "mlp: parameter count mismatch");
   const float* const given = params;  // the finiteness scan (range guard) reads the caller's values
   const int H = wmax <= 16 ? 16 : wmax <= 32 ? 32 : wmax <= 64 ? 64 : 128;
-  const int nx = n_in - 1, nxp = (nx + 15) & ~15, L = n_hidden;
+  const int nx = n_in - 1, L = n_hidden;
+  // nx padded to 16 (the fp32 weight images) and to 32 (the split ones).  The split layer-1 rows are
+  // LDS chunks of at most 128 words whose 16-B granules are XOR-swizzled by row (split_swz): a closed
+  // permutation only for 8, 16 or 32 granules per row, so a chunk of 96 words (nx in 65..96, or
+  // 193..224 in the wide instances) is padded to 128 with zero columns — and nxp with it, so the path
+  // kernels zero those rows of their noise tile (and the fp32 images carry the same zero columns)
+  int nxp = (nx + 15) & ~15, nxp32 = (nx + 31) & ~31;
+  if ((nxp32 & 127) == 96) nxp = nxp32 = nxp32 + 32;
   std::vector<float> padded;
   bool same = true;
   for (int l = 0; l < n_hidden; ++l) same = same && widths[l] == H;
@@ -800,11 +807,6 @@ int dpi_net_create_mlp(int n_in, int n_hidden, const int* widths, int act, const
   for (int h = 0; h < H; ++h) blob[owout + h] = cur[h];
   const float bout = cur[H];
   // fp16-split copies for the split MFMA path (H % 32 == 0)
-  // the split layer-1 rows are LDS chunks of at most 128 words whose 16-B granules are XOR-swizzled
-  // by row (split_swz): a closed permutation only for 8, 16 or 32 granules per row, so a chunk of 96
-  // words (nx in 65..96, or 193..224 in the wide instances) is padded to 128 with zero columns
-  int nxp32 = (nx + 31) & ~31;
-  if ((nxp32 & 127) == 96) nxp32 += 32;
   size_t oW1xS = 0, oW1xTS = 0, oWS[4] = {0}, oWTS[4] = {0}, oWU[4] = {0};
   float wus[4] = {1.f, 1.f, 1.f, 1.f};
   int ea[4] = {0, 0, 0, 0}, eb[4] = {0, 0, 0, 0};  // mlp_hdiag_split's operand exponents
