@@ -2,7 +2,7 @@
 # One GPU call of a round, by stages: GPU tests, bench lines for every workload, kernel traces (one
 # stream for HJB), the counter list, the VALU / HBM PMC passes, same-box A/B against the round-5
 # package (ab, probe: tools/variants/r05pkg), the N = 2 gloo rehearsals and the RCCL smoke.
-# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
+# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|wide|gbmlong|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
 #        outputs under gpurun_out/<tag>/
 set -e
 tag=${1:-r02}; shift || true
@@ -34,6 +34,10 @@ for w in $what; do
     DPI_FUSED_BASE=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_burgers_fb0 -o trace \
       --output-format csv -- python bench.py --workload burgers --steps 10 --warmup 2 --no-cpu-baseline \
       > $out/trace_burgers_fb0.log 2>&1 ;;
+  wide)  # not a BASELINE config: the configs[1] network at nx = 256
+    run 300 $out/bench_burgers_nx256.log python bench.py --workload burgers_nx256 --no-cpu-baseline ;;
+  gbmlong)  # GBM over 60 steps (15 timed launches for kernel_ms)
+    run 300 $out/bench_gbm_60.log python bench.py --workload gbm --steps 60 --warmup 3 --no-cpu-baseline ;;
   hjb)
     run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
@@ -60,16 +64,20 @@ for w in $what; do
       --master-port 29511 tools/nccl_smoke.py ;;
   counters)
     timeout -k 10 120 rocprofv3 -L > $out/counters.txt 2>&1 ;;
+  pmcgbm)  # the GBM VALU pass alone (network launch + the prepare stream's k_noise_shared)
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+      --kernel-include-regex "k_paths|k_noise" -d $out/pmc_valu_gbm -o pmc --output-format csv -- \
+      python bench.py --workload gbm --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu_gbm.log 2>&1 ;;
   pmc)
     for wl in burgers burgers_cfg3 gbm gbm_hess; do
       timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-        --kernel-include-regex k_paths -d $out/pmc_valu_$wl -o pmc --output-format csv -- \
+        --kernel-include-regex "k_paths|k_noise" -d $out/pmc_valu_$wl -o pmc --output-format csv -- \
         python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_valu_$wl.log 2>&1
     done
     for wl in burgers burgers_cfg3 hjb gbm gbm_hess; do
       for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm|k_reduce" -d $out/pmc_${wl}_$c -o pmc \
-          --output-format csv -- python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline > $out/pmc_${wl}_$c.log 2>&1
+        timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "k_paths|k_pis|k_gemm|k_reduce|k_noise" -d $out/pmc_${wl}_$c -o pmc \
+          --output-format csv -- python bench.py --workload $wl --steps 10 --warmup 2 --no-cpu-baseline --no-fp32-pass > $out/pmc_${wl}_$c.log 2>&1
       done
     done ;;
   esac
