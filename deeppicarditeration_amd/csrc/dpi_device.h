@@ -59,6 +59,10 @@ constexpr int WST = 136;           // LDS row stride of a staged weight chunk (W
 #ifndef DPI_GBM_WAGPR
 #define DPI_GBM_WAGPR 1
 #endif
+// the GBM network launch's wave index through readfirstlane (paths_body; an A/B knob)
+#ifndef DPI_WV_UNIFORM_GBM
+#define DPI_WV_UNIFORM_GBM 0
+#endif
 #ifndef DPI_NOISE_UNROLL_HESS
 // the Hessian-label k_paths: 1 -> 4 r04o (same-box A/B, 2 pairs: 1.747 -> 1.719 ms/step)
 #define DPI_NOISE_UNROLL_HESS 4
@@ -1910,14 +1914,7 @@ __device__ __forceinline__ void noise_task(const PathArgs& a, int nb, int t) {
   if (!(a.flags & (part ? DPI_INTEGRAL : DPI_TERMINAL))) return;
   for (int j = wq; j < nb; j += 4) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll UNR
-    for (int k = 0; k < a.K; ++k) {
-      const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3, a.k0, a.k1));
-      s0 += z.a;
-      s1 += z.b;
-      s2 += z.c;
-      s3 += z.d;
-    }
+    noise_sums<UNR>(a.K, nb, j, m, ig, c3, a.k0, a.k1, s0, s1, s2, s3);
     out[(4 * j + 0) * P] = s0 * BM_SCALE;
     out[(4 * j + 1) * P] = s1 * BM_SCALE;
     out[(4 * j + 2) * P] = s2 * BM_SCALE;
@@ -2267,7 +2264,15 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   constexpr int NOISE_UNROLL = HESS ? DPI_NOISE_UNROLL_HESS
                                : GBM ? (ZERO ? 4 : DPI_NOISE_UNROLL_GBM)
                                      : DPI_NOISE_UNROLL_FO;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr bool NOISE_WU = false;  // the plain philox4x32_10 (see wv below)
+  // The wave index as the compiler sees it: divergent (tid >> 6), so the dim-block indices j and the
+  // Philox counter words c0 = k nb + j live in VGPRs.  Made uniform (readfirstlane) with the
+  // scalar-unit Philox (philox4x32_10_wu), the noise loop issues 195 instead of 216 VALU instructions
+  // per 4 calls but 61 SALU more, and two waves per SIMD then issue slower: Burgers 0.360 -> 0.388
+  // ms/step, Hessian labels 1.750 -> 1.784 (same-box A/B, profiles/r06o_ab); kept for the one-wave
+  // k_noise_shared only.  DPI_WV_UNIFORM_GBM: the A/B knob for the GBM network launch.
+  constexpr bool WV_UNIFORM = DPI_WV_UNIFORM_GBM && GBM && !HESS && !TD && NXW == NXP_MAX;
+  const int tid = threadIdx.x, lane = tid & 63, wv = WV_UNIFORM ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const uint32_t ig = a.point_base + (uint32_t)i;
   const uint32_t m = (uint32_t)(a.m_begin + P * blk + lane);
   const int nx = e.nx, F = 1 + nx;
@@ -2403,14 +2408,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
           for (int q = 0; q < 4; ++q) ST[c][q] = np[(4 * j + q) * P];
         } else {
           float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-          #pragma unroll NOISE_UNROLL
-          for (int k = 0; k < a.K; ++k) {
-            const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3t, a.k0, a.k1));
-            s0 += z.a;
-            s1 += z.b;
-            s2 += z.c;
-            s3 += z.d;
-          }
+          noise_sums<NOISE_UNROLL, NOISE_WU>(a.K, nb, j, m, ig, a.c3t, a.k0, a.k1, s0, s1, s2, s3);
           ST[c][0] = s0 * BM_SCALE;
           ST[c][1] = s1 * BM_SCALE;
           ST[c][2] = s2 * BM_SCALE;
@@ -2431,14 +2429,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
       if (j < nb) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
         if (INTG && !PRE) {
-          #pragma unroll NOISE_UNROLL
-          for (int k = 0; k < a.K; ++k) {
-            const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, a.c3i, a.k0, a.k1));
-            s0 += z.a;
-            s1 += z.b;
-            s2 += z.c;
-            s3 += z.d;
-          }
+          noise_sums<NOISE_UNROLL, NOISE_WU>(a.K, nb, j, m, ig, a.c3i, a.k0, a.k1, s0, s1, s2, s3);
         }
         float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
         if (INTG && PRE) {  // rolled out by k_noise_shared (GBM prepared calls)

@@ -126,7 +126,13 @@ __device__ __forceinline__ void pis_put4(float* dst, const float (&v)[4], int d0
 // block on the prepare stream (dpi_label_prepare).
 constexpr int PIS_PARTS = 4;
 constexpr int PIS_GST = 8;  // SC + PIS_GST + NSG q: terminal GMM statistics of part q
-template <int KIND, bool X3, int UNR>
+// WU: the scalar-unit Philox (philox4x32_10_wu; DPI_PIS_WU=1).  Off: the one-stream rollout measured
+// even (HJB 3.711 / 3.714 vs 3.729 / 3.712 ms/step, r06o_ab) and under the shared wave's 48-register cap
+// the scalar form spilled 9 VGPRs.
+#ifndef DPI_PIS_WU
+#define DPI_PIS_WU 0
+#endif
+template <int KIND, bool X3, int UNR, bool WU = DPI_PIS_WU>
 __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
                                                  uint32_t k1, uint32_t c3t, uint32_t c3s, uint32_t c3i,
@@ -156,15 +162,7 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
     for (int c = 0; c < NSG; ++c) gst[c] = 0.f;
     for (int j = j0; j < j1; ++j) {
       float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-      if (TERM)
-#pragma unroll UNR
-        for (int k = 0; k < K; ++k) {
-          const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3t, k0, k1));
-          s0 += z.a;
-          s1 += z.b;
-          s2 += z.c;
-          s3 += z.d;
-        }
+      if (TERM) noise_sums<UNR, WU>(K, nb, j, m, ig, c3t, k0, k1, s0, s1, s2, s3);
       const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
       float xv[4];
 #pragma unroll
@@ -204,15 +202,7 @@ __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev
   const float cI = e.asq * sqrtf(smt / Kf);
   for (int j = j0; j < j1; ++j) {
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    if (INTG)
-#pragma unroll UNR
-      for (int k = 0; k < K; ++k) {
-        const f4 z = normals4_raw(philox4x32_10((uint32_t)(k * nb + j), m, ig, c3i, k0, k1));
-        s0 += z.a;
-        s1 += z.b;
-        s2 += z.c;
-        s3 += z.d;
-      }
+    if (INTG) noise_sums<UNR, WU>(K, nb, j, m, ig, c3i, k0, k1, s0, s1, s2, s3);
     const float sv[4] = {s0 * BM_SCALE, s1 * BM_SCALE, s2 * BM_SCALE, s3 * BM_SCALE};
     float xv[4];
 #pragma unroll
@@ -290,7 +280,7 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
     if (lane == 0) t = atomicAdd(queue, 1);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= ntask) break;
-    pis_rollout_wave<KIND, X3, UNR>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
+    pis_rollout_wave<KIND, X3, UNR, false>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
                                     stage, td_dt, bx0 + t / (2 * PIS_PARTS), t % (2 * PIS_PARTS));
   }
 }
