@@ -132,6 +132,9 @@ constexpr int PIS_GST = 8;  // SC + PIS_GST + NSG q: terminal GMM statistics of 
 #ifndef DPI_PIS_WU
 #define DPI_PIS_WU 0
 #endif
+#ifndef DPI_PIS_SHARED_WU  // the same for the shared rollout wave (an A/B knob; at 4 chains it spills)
+#define DPI_PIS_SHARED_WU 0
+#endif
 template <int KIND, bool X3, int UNR, bool WU = DPI_PIS_WU>
 __device__ __forceinline__ void pis_rollout_wave(const EqDev& e, const NetPisDev& pn, const float* __restrict__ tx,
                                                  int g0, int nbp, int m_begin, int K, int flags, uint32_t k0,
@@ -280,7 +283,7 @@ __device__ __forceinline__ void pis_rollout_shared_body(EqDev e, NetPisDev pn, c
     if (lane == 0) t = atomicAdd(queue, 1);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= ntask) break;
-    pis_rollout_wave<KIND, X3, UNR, false>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
+    pis_rollout_wave<KIND, X3, UNR, DPI_PIS_SHARED_WU>(e, pn, tx, g0, nbp, m_begin, K, flags, k0, k1, c3t, c3s, c3i, point_base, rows, L,
                                     stage, td_dt, bx0 + t / (2 * PIS_PARTS), t % (2 * PIS_PARTS));
   }
 }
