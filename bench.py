@@ -251,6 +251,8 @@ def main():
     # one wave per SIMD (k_pis_rollout_shared) — the default for that workload
     # GBM (configs[4], first-order labels): the next batch's noise sums (k_noise_shared, one wave per
     # SIMD) beside this batch's network launch — 0.768 -> 0.735 ms/step (profiles/r05d_bench_gbm_*)
+    # (GBM Hessian labels: `--prepare` stages the next batch's noise sums the same way — bitwise the same
+    # labels but slower, 1.88-1.94 against 1.74-1.75 ms/step one-stream, profiles/r06s_hessab; not the default)
     args.prepare = (args.prepare or bool(WORKLOADS[args.workload].get("pis") or args.workload == "gbm")) \
         and not args.no_prepare
     if args.prepare and os.environ.get("DPI_BENCH_MAIN_PRIORITY", "high") == "high":
@@ -342,6 +344,11 @@ def main():
             begun.append(prep[:2])
             pending.append(labeler.begin(prepared=prep, on_moments_begin=rec0, on_moments_end=rec1))
             return finish(pending.pop(0)) if len(pending) > 1 else None
+        if wl.get("hess") and args.prepare:  # the next batch's points, baseline and noise sums on the side stream
+            prep = labeler.prepare(N_POINTS, hessians=True)
+            begun.append(prep[:2])
+            pending.append(("hess", labeler.labels_hessians(prepared=prep, on_moments_begin=rec0, on_moments_end=rec1)))
+            return finish(pending.pop(0))
         if not wl.get("hess") and not pipelined:  # one rank: sampling inside the path launch (one launch)
             tx, pb, y = labeler.sample_labels(N_POINTS, on_moments_begin=rec0, on_moments_end=rec1)
             begun.append((tx, pb))
@@ -572,6 +579,8 @@ def main():
                                          "fp32 accumulator, DESIGN.md §2.2)")),
                        "process_group": None if dist is None else backend + (" (ranks share cuda:0)" if share else ""),
                        "schedule": ("two-phase, next batch prepared on a side stream" if args.prepare and pipelined
+                                    else "next batch's points, baseline and noise sums prepared on a side stream"
+                                    if args.prepare and wl.get("hess")
                                     else "two-phase (all-gather overlapped)" if pipelined else "one labels() call"),
                        "prewarm_steps": prewarm,
                        "range_check": args.range_check != "off",

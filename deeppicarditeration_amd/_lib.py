@@ -10,7 +10,7 @@ _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("DPI_HIP_LIB", _HERE / "libdpi_hip.so"))
 
 # constants mirrored from include/dpi.h (checked against the header by tests/test_capi.py)
-DPI_ABI_VERSION = 6
+DPI_ABI_VERSION = 7
 DPI_LAUNCH_TIMERS = 256  # include/dpi.h
 DPI_OK, DPI_ERR_ARG, DPI_ERR_UNSUPPORTED, DPI_ERR_HIP, DPI_ERR_WORKSPACE = 0, -1, -2, -3, -4
 DPI_TAG_T, DPI_TAG_X0, DPI_TAG_X, DPI_TAG_TERM, DPI_TAG_S, DPI_TAG_INT, DPI_TAG_SDGD, DPI_TAG_HTERM, DPI_TAG_HINT = range(1, 10)
@@ -76,6 +76,7 @@ SIGNATURES = {
     "dpi_sample_points_baseline": (c_int, [c_void_p, c_void_p, c_int, c_uint64, c_uint32, c_uint32, c_float, c_int,
                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "dpi_workspace_bytes_hessians": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
+    "dpi_workspace_bytes_hessians_prepared": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_label_moments_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
                                            c_uint32, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                            c_void_p]),

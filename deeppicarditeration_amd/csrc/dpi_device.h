@@ -2297,7 +2297,7 @@ __device__ __forceinline__ void paths_body(const EqDev& e, const NetDev& net, co
   }
   const float Kf = (float)a.K;
   // GBM prepared calls: phase 1's noise sums come from k_noise_shared (a wave-uniform branch)
-  const bool PRE = GBM && !HESS && !TD && a.noise != nullptr;
+  const bool PRE = GBM && !TD && a.noise != nullptr;  // first-order and Hessian labels
 
   if (FB) {
     if (tid < nb) {

@@ -2221,6 +2221,12 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M) {
   size_t moff;
   return al256(ws_layout(net, n, M, 1 + p->e.nx).total) + hess_extra(n, M, p->e.nx, &moff);
 }
+// the same with the GBM noise staging region (dpi_label_prepare + a DPI_PREPARED Hessian-label call)
+size_t dpi_workspace_bytes_hessians_prepared(dpi_problem p, dpi_net net, int n, int M) {
+  if (!p || n < 0 || M < 0) return 0;
+  size_t moff;
+  return al256(ws_layout(net, n, M, 1 + p->e.nx, gbm_noise_prep(p, net)).total) + hess_extra(n, M, p->e.nx, &moff);
+}
 
 static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                              uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
@@ -2231,16 +2237,22 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
     return fail(DPI_ERR_UNSUPPORTED, "Hessian labels need a SimpleDiffusionEquationWithHessian (GBMEquationComplexExact)");
   if (net->d.kind == 2) return fail(DPI_ERR_UNSUPPORTED, "Hessian labels: MLP or ZeroSolution networks only");
   if (n < 0 || (n && (!tx || !ws || !moments)) || K < 1 || M < 1 || m_begin < 0 || m_end > M || m_end <= m_begin ||
-      (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu || !(flags & DPI_BOTH) || (flags & ~DPI_BOTH))
+      (m_begin % P) || (m_end % P) || epoch > 0xFFFFFFu || !(flags & DPI_BOTH) || (flags & ~(DPI_BOTH | DPI_PREPARED)))
     return fail(DPI_ERR_ARG, "Hessian labels: bad arguments (m range multiple of 64 within [0, M], K >= 1, flags in "
-                             "DPI_TERMINAL | DPI_INTEGRAL)");
+                             "DPI_TERMINAL | DPI_INTEGRAL | DPI_PREPARED)");
   if (n == 0) return 0;
   const int nx = p->e.nx, F = 1 + nx, C = nx * nx, nbp = (m_end - m_begin) / P;
   if (nbp > DPI_PATHS_PER_CALL_MAX / P) return fail(DPI_ERR_ARG, "Hessian labels: at most DPI_PATHS_PER_CALL_MAX paths per call");
-  const WsLayout w = ws_layout(net, n, M, F);
+  // a prepared call (GBM): the terminal / integral noise sums were staged by dpi_label_prepare's
+  // k_noise_shared in the prepared layout's noise region — the same counters and summation order as
+  // the path launch's own rollout, so the labels are bitwise the unprepared call's
+  const bool staged = (flags & DPI_PREPARED) && gbm_noise_prep(p, net);
+  const WsLayout w = ws_layout(net, n, M, F, staged);
   size_t moff;
   const size_t base = al256(w.total), need = base + hess_extra(n, M, nx, &moff);
-  if (ws_bytes < need) return fail(DPI_ERR_WORKSPACE, "workspace too small (dpi_workspace_bytes_hessians)");
+  if (ws_bytes < need)
+    return fail(DPI_ERR_WORKSPACE, staged ? "workspace too small (dpi_workspace_bytes_hessians_prepared)"
+                                          : "workspace too small (dpi_workspace_bytes_hessians)");
   char* b = (char*)ws;
   PathArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -2254,7 +2266,8 @@ static int hess_moments_impl(dpi_problem p, dpi_net net, const float* tx, int n,
   a.nbp = nbp;
   a.m_begin = m_begin;
   a.K = K;
-  a.flags = flags;
+  a.flags = flags & DPI_BOTH;
+  if (staged) a.noise = (const float*)(b + w.noise);
   a.k0 = (uint32_t)seed;
   a.k1 = (uint32_t)(seed >> 32);
   a.c3t = DPI_TAG_TERM | (epoch << 8);
@@ -2289,6 +2302,8 @@ int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int 
                                uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                                float* hessian_sums, void* ws, size_t ws_bytes, void* stream) {
   if (!hessian_sums) return fail(DPI_ERR_ARG, "label_moments_hessians: null hessian_sums");
+  int rc = check_prepared(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, ws, ws_bytes);
+  if (rc) return rc;
   return hess_moments_impl(p, net, tx, n, M, K, seed, epoch, point_base, m_begin, m_end, flags, moments, hessian_sums,
                            ws, ws_bytes, stream, nullptr, 0.f);
 }

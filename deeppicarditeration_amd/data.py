@@ -585,7 +585,8 @@ class OnlineDataGenerator:
         fn = self.lib.dpi_workspace_bytes_prepared if prepared else self.lib.dpi_workspace_bytes
         need = fn(self.problem, self.net.handle, n, M)
         if hessians:
-            need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
+            fh = self.lib.dpi_workspace_bytes_hessians_prepared if prepared else self.lib.dpi_workspace_bytes_hessians
+            need = max(need, fh(self.problem, self.net.handle, n, M))
         return need
 
     def point_baseline(self, tx, hessians=False, ws=None):
@@ -661,7 +662,7 @@ class OnlineDataGenerator:
         """Hessian-label sums over m in [m_begin, m_end): moments (n, 2, 1+nx), Hessian sums (n, nx^2),
         of the estimators `flags` selects (DPI_TERMINAL / DPI_INTEGRAL / both).  More than
         PATHS_PER_CALL_MAX paths run as several calls combined by sums_reduce."""
-        pieces = self._pieces(m_begin, m_end)
+        pieces = self._pieces(m_begin, m_end, flags)
         if len(pieces) > 1:
             parts = [self._label_moments_hessians(tx, point_base, M, a, b, ws, flags) for a, b in pieces]
             return (self.sums_reduce(torch.stack([p[0] for p in parts])),

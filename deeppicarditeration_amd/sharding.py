@@ -128,23 +128,44 @@ class ShardedLabeler:
         g = getattr(self.gen, "_guarded", None)
         return call() if g is None else g(call, reduce_flag=self._reduce_flag)
 
-    def labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
-        return self._guarded(lambda: self._labels_hessians(tx, point_base, on_moments_begin, on_moments_end))
+    def labels_hessians(self, tx=None, point_base=None, on_moments_begin=None, on_moments_end=None, prepared=None):
+        """Hessian labels of tx, or of the batch prepare(n, hessians=True) returned (`prepared`: its
+        points, baseline and staged noise sums; the labels are bitwise those of the unprepared call).
+        A range-guard repair reruns the batch unprepared."""
+        if prepared is not None:
+            tx, point_base = prepared[0], prepared[1]
+        state = {"prep": prepared}
 
-    def _labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None):
+        def call():
+            prep, state["prep"] = state["prep"], None
+            return self._labels_hessians(tx, point_base, on_moments_begin, on_moments_end, prep)
+        return self._guarded(call)
+
+    def _labels_hessians(self, tx, point_base, on_moments_begin=None, on_moments_end=None, prepared=None):
         """generate_with_gradients_and_hessians for tx with this rank's MC shard (n, 1 + nx + nx^2);
         identical on every rank.  Exchange: the (n, 2, 1+nx) moments and (n, nx^2) Hessian sums (of
         both estimator passes when n_estimate_terminal != n_estimate_integral)."""
+        from . import _lib
         sets = self.estimator_sets()
-        ws = self.gen.point_baseline(tx, hessians=True)
+        kflags = 0
+        if prepared is not None:
+            _, _, ws, ready, slot, _, staged = prepared
+            torch.cuda.current_stream(self.gen.device).wait_event(ready)
+            if staged:
+                kflags = _lib.DPI_PREPARED
+        else:
+            ws = self.gen.point_baseline(tx, hessians=True)
         if on_moments_begin:
             on_moments_begin()
         if len(sets) == 1:
             M = sets[0][0]
-            mom, hs = self.gen.label_moments_hessians(tx, point_base, M, *self.shard(M), ws)
+            mom, hs = self.gen.label_moments_hessians(tx, point_base, M, *self.shard(M), ws,
+                                                      flags=_lib.DPI_BOTH | kflags)
             if on_moments_end:
                 on_moments_end()
-            return self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
+            y = self.gen.finalize_hessians(self.gather_sums(mom), self.gather_sums(hs), M, ws)
+            self._release_prepared(prepared)
+            return y
         sums = [self.gen.label_moments_hessians(tx, point_base, M, *self.shard(M), ws, flags=f) for M, f in sets]
         if on_moments_end:
             on_moments_end()
@@ -152,17 +173,30 @@ class ShardedLabeler:
             moms = self._gather_stacked([m for m, _ in sums], self.gen.sums_reduce)
             hss = self._gather_stacked([h for _, h in sums], self.gen.sums_reduce)
             sums = list(zip(moms, hss))
-        return self._add_clip([self.gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"), flags=f)
-                               for (mom, hs), (M, f) in zip(sums, sets)])
+        y = self._add_clip([self.gen.finalize_hessians(mom, hs, M, ws, bound=float("inf"), flags=f)
+                            for (mom, hs), (M, f) in zip(sums, sets)])
+        self._release_prepared(prepared)
+        return y
+
+    def _release_prepared(self, prepared):
+        """prepare() may refill a prepared batch's workspace once the work enqueued on it has run."""
+        if prepared is None:
+            return
+        slot = prepared[4]
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(self.gen.device))
+        self._prep_free[slot] = done
+        self._prep_busy[slot] = False
 
     # ------------------------------------------------------------------ two-phase (pipelined) labels
-    def prepare(self, n, flags=None):
+    def prepare(self, n, flags=None, hessians=False):
         """Sample the next batch's points, their per-point baseline and (PISGradNet) the first path
         chunk's rollout on a side stream, into one of three workspaces, so they run while the
         current stream still executes the previous batch's moments: the baseline is a handful of
         latency-bound blocks that otherwise serialise between two path launches, and the VALU-bound
         rollout fits on each CU beside a k_gemm_x3 block of the previous batch's MFMA-bound GEMM
-        chain.  Returns the handle for begin(prepared=...)."""
+        chain.  Returns the handle for begin(prepared=...), or, with hessians=True (workspaces sized
+        for the Hessian labels), for labels_hessians(prepared=...)."""
         from . import _lib
         flags = _lib.DPI_BOTH if flags is None else flags
         gen = self.gen
@@ -172,7 +206,7 @@ class ShardedLabeler:
         # unequal estimator counts run two label passes in begin(): their points and baseline are
         # prepared here, the passes themselves are not staged
         staged = len(sets) == 1
-        need = gen.workspace_bytes(n, M, prepared=True)
+        need = gen.workspace_bytes(n, M, hessians=hessians, prepared=True)
         if getattr(self, "_prep_ws", None) is None or self._prep_ws[0].numel() < need:
             torch.cuda.synchronize(gen.device)  # a resized pool must not alias in-flight work
             self._side = torch.cuda.Stream(device=gen.device)

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DPI_ABI_VERSION 6
+#define DPI_ABI_VERSION 7
 
 /* error codes */
 #define DPI_OK 0
@@ -299,6 +299,9 @@ int dpi_sample_points_baseline(dpi_problem p, dpi_net net, int n, uint64_t seed,
  * Noise: the first-order streams plus N1 = tag DPI_TAG_HTERM, N2 = tag DPI_TAG_HINT (k = 0).
  * ws >= dpi_workspace_bytes_hessians(p, net, n, M). */
 size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
+/* ws of a dpi_label_prepare + DPI_PREPARED dpi_label_moments_hessians pair (GBM MLP nets: the
+ * terminal / integral noise sums staged by the prepare, as for first-order labels); ABI 7. */
+size_t dpi_workspace_bytes_hessians_prepared(dpi_problem p, dpi_net net, int n, int M);
 
 /* Sharding building blocks of the Hessian labels (the first-order dpi_label_moments pattern):
  * after dpi_point_baseline, the sums over m in [m_begin, m_end) of the value/gradient
@@ -308,7 +311,9 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
  * select the estimators (terminal: value/gradient + N1 Hessian term and its identity part, + g(x) at
  * finalize; integral: the same for f and N2), so n_estimate_terminal != n_estimate_integral runs as
  * a DPI_TERMINAL pass over M_T paths plus a DPI_INTEGRAL pass over M_I paths, summed
- * (picard/data.py:1164 vs :845). */
+ * (picard/data.py:1164 vs :845).  flags may include DPI_PREPARED (ABI 7): a dpi_label_prepare with the
+ * same arguments ran on this workspace (sized by dpi_workspace_bytes_hessians_prepared), and the
+ * labels are bitwise those of the unprepared call. */
 int dpi_label_moments_hessians(dpi_problem p, dpi_net net, const float* tx, int n, int M, int K, uint64_t seed,
                                uint32_t epoch, uint32_t point_base, int m_begin, int m_end, int flags, float* moments,
                                float* hessian_sums, void* ws, size_t ws_bytes, void* stream);

@@ -598,6 +598,39 @@ def test_side_stream_preparation_equals_labels(kind):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["split", "f32"])
+def test_side_stream_preparation_equals_hessian_labels(precision):
+    """bench.py --workload gbm_hess: ShardedLabeler.prepare(n, hessians=True) (sampling, per-point
+    baseline and the k_noise_shared noise sums on a side stream, two batches prepared ahead) ->
+    labels_hessians(prepared=...) gives every batch's Hessian labels bit for bit as the unprepared
+    call on the same points (the staged sums are the path launch's own, same counters and order)."""
+    import deeppicarditeration_amd as dpi
+    from deeppicarditeration_amd.sharding import ShardedLabeler
+
+    def make():
+        eq = dpi.GBMEquationComplexExact(100, 1.0, 1.0)
+        torch.manual_seed(4)
+        net = dpi.construct_mlp(101, 1, [64] * 3, ["ELU"] * 3, None)
+        gen = dpi.OnlineDataGenerator(eq, net, 1, 1, device="cuda:0", t_always_uniform=True, n_estimate_terminal=256,
+                                      n_estimate_integral=256, n_euler_steps=6, seed=3)
+        if precision == "f32":
+            gen.net.set_precision(0)
+        return gen
+
+    lab, ref = ShardedLabeler(make()), ShardedLabeler(make())
+    got, prep = [], lab.prepare(8, hessians=True)
+    for _ in range(5):
+        nxt = lab.prepare(8, hessians=True)
+        got.append(lab.labels_hessians(prepared=prep))
+        prep = nxt
+    got.append(lab.labels_hessians(prepared=prep))
+    torch.cuda.synchronize()
+    for y in got:
+        tx, pb = ref.gen.sample_t_and_x(8)
+        assert torch.equal(y, ref.labels_hessians(tx, pb))
+
+
+@pytest.mark.gpu
 def test_prepared_moments_check_the_prepare_call():
     """include/dpi.h DPI_PREPARED contract: a prepared moments call whose points, counters or MC
     range differ from the dpi_label_prepare call on its workspace, or that has no prepare (a second

@@ -2,7 +2,7 @@
 # One GPU call of a round, by stages: GPU tests, bench lines for every workload, kernel traces (one
 # stream for HJB), the counter list, the VALU / HBM PMC passes, same-box A/B against the round-5
 # package (ab, probe: tools/variants/r05pkg), the N = 2 gloo rehearsals and the RCCL smoke.
-# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|wide|gbmlong|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
+# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|wide|gbmlong|hessab|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
 #        outputs under gpurun_out/<tag>/
 set -e
 tag=${1:-r02}; shift || true
@@ -38,6 +38,11 @@ for w in $what; do
     run 300 $out/bench_burgers_nx256.log python bench.py --workload burgers_nx256 --no-cpu-baseline ;;
   gbmlong)  # GBM over 60 steps (15 timed launches for kernel_ms)
     run 300 $out/bench_gbm_60.log python bench.py --workload gbm --steps 60 --warmup 3 --no-cpu-baseline ;;
+  hessab)  # Hessian labels: the prepare schedule against one stream, interleaved
+    for r in 1 2; do
+      run 300 $out/bench_gbm_hess_prep_$r.log python bench.py --workload gbm_hess --steps 40 --warmup 3 --no-cpu-baseline --no-fp32-pass --prepare
+      run 300 $out/bench_gbm_hess_plain_$r.log python bench.py --workload gbm_hess --steps 40 --warmup 3 --no-cpu-baseline --no-fp32-pass
+    done ;;
   hjb)
     run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_hjb_onestream -o trace --output-format csv -- \
