@@ -77,6 +77,7 @@ SIGNATURES = {
                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "dpi_workspace_bytes_hessians": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
     "dpi_workspace_bytes_hessians_prepared": (c_size_t, [c_void_p, c_void_p, c_int, c_int]),
+    "dpi_workspace_forget": (c_int, [c_void_p, c_size_t]),
     "dpi_label_moments_hessians": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_uint64, c_uint32,
                                            c_uint32, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                            c_void_p]),

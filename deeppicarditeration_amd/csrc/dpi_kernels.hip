@@ -2077,6 +2077,18 @@ static void prep_tags_drop(const void* owner) {
     it = (it->second.p == owner || it->second.net == owner) ? prep_tags().erase(it) : std::next(it);
 }
 
+extern "C" int dpi_workspace_forget(const void* ws, size_t ws_bytes) {
+  const char *lo = (const char*)ws, *hi = lo + ws_bytes;
+  auto inside = [&](const void* a) { return (const char*)a >= lo && (const char*)a < hi; };
+  {
+    std::lock_guard<std::mutex> g(g_base_mu);
+    for (auto it = base_tags().begin(); it != base_tags().end();) it = inside(it->first) ? base_tags().erase(it) : std::next(it);
+  }
+  std::lock_guard<std::mutex> g(g_prep_mu);
+  for (auto it = prep_tags().begin(); it != prep_tags().end();) it = inside(it->first) ? prep_tags().erase(it) : std::next(it);
+  return 0;
+}
+
 static bool stages_prepare(dpi_problem p, dpi_net net) {
   return (net->d.kind == 2 || gbm_noise_prep(p, net)) && !(p->td_dt > 0.f);
 }

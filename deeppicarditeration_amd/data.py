@@ -41,6 +41,16 @@ def _stream(device):
     return _lib.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def new_workspace(nbytes, device):
+    """A label-call workspace (uint8).  The caching allocator may hand out a freed workspace's
+    address: the library's host-side records of that address (a baseline's fused-reduce tag, an
+    unconsumed prepare) are dropped (dpi_workspace_forget), so they cannot vouch for the new one."""
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    if ws.is_cuda:
+        _lib.check(_lib.load().dpi_workspace_forget(_ptr(ws), ws.numel()), "dpi_workspace_forget")
+    return ws
+
+
 class SplitRangeWarning(RuntimeWarning):
     """A network's fp16-split evaluation left fp16's range: its labels are recomputed, and the
     generator's later calls made, with exact-fp32 MFMA (DPI_GEMM_F32) for that network."""
@@ -404,7 +414,7 @@ class OnlineDataGenerator:
         if hessians:
             need = max(need, self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M))
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self._device)
+            self._ws = new_workspace(need, self._device)
         return self._ws
 
     def _take_points(self, n):
@@ -770,7 +780,7 @@ class OnlineDataGenerator:
             return self.finalize_hessians(mom, hs, M, ws, bound)
         need = self.lib.dpi_workspace_bytes_hessians(self.problem, self.net.handle, n, M)
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self._device)
+            self._ws = new_workspace(need, self._device)
         y = torch.empty(n, 1 + nx + nx * nx, dtype=torch.float32, device=self._device)
         self._configure_problem()
         _lib.check(self.lib.dpi_generate_with_gradients_and_hessians(

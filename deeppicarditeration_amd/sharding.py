@@ -210,7 +210,8 @@ class ShardedLabeler:
         if getattr(self, "_prep_ws", None) is None or self._prep_ws[0].numel() < need:
             torch.cuda.synchronize(gen.device)  # a resized pool must not alias in-flight work
             self._side = torch.cuda.Stream(device=gen.device)
-            self._prep_ws = [torch.empty(need, dtype=torch.uint8, device=gen.device) for _ in range(3)]
+            from .data import new_workspace
+            self._prep_ws = [new_workspace(need, gen.device) for _ in range(3)]
             self._prep_free, self._prep_next, self._prep_busy = [None] * 3, 0, [False] * 3
         k = self._prep_next
         if self._prep_busy[k]:
@@ -291,7 +292,8 @@ class ShardedLabeler:
                 if any(getattr(self, "_ws_busy", ())):
                     raise RuntimeError("begin(): cannot resize the workspaces while a batch is pending")
                 dev = getattr(tx, "device", "cpu")
-                self._ws_pool = [torch.empty(need, dtype=torch.uint8, device=dev) for _ in range(2)]
+                from .data import new_workspace
+                self._ws_pool = [new_workspace(need, dev) for _ in range(2)]
                 self._ws_next, self._ws_busy = 0, [False, False]
             wslot = self._ws_next
             if self._ws_busy[wslot]:

@@ -303,6 +303,13 @@ size_t dpi_workspace_bytes_hessians(dpi_problem p, dpi_net net, int n, int M);
  * terminal / integral noise sums staged by the prepare, as for first-order labels); ABI 7. */
 size_t dpi_workspace_bytes_hessians_prepared(dpi_problem p, dpi_net net, int n, int M);
 
+/* The library keeps host-side records per workspace address: the fused reduce's "a baseline of n
+ * points was enqueued here" tag (dpi_point_baseline / dpi_sample_points_baseline, checked by
+ * dpi_label_moments) and an unconsumed dpi_label_prepare.  A caller that frees a workspace and
+ * allocates another (a caching allocator may return the same address) calls this on the new range
+ * [ws, ws + ws_bytes) so the old records cannot vouch for it.  Host only, no device work; ABI 7. */
+int dpi_workspace_forget(const void* ws, size_t ws_bytes);
+
 /* Sharding building blocks of the Hessian labels (the first-order dpi_label_moments pattern):
  * after dpi_point_baseline, the sums over m in [m_begin, m_end) of the value/gradient
  * contributions and their squares (moments (n, 2, 1+nx)) and of the Hessian contributions

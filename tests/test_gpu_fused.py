@@ -210,3 +210,27 @@ def test_fused_label_call_without_a_baseline_on_its_workspace_fails():
     gen.point_baseline(tx, ws=ws)
     y, _ = gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, ws)
     assert torch.isfinite(y).all()
+
+
+@pytest.mark.gpu
+def test_a_reused_workspace_address_loses_its_baseline_tag():
+    """the fused reduce's baseline tag is keyed on the workspace address, which the
+    caching allocator hands out again.  dpi_workspace_forget (called by new_workspace on every
+    workspace the package allocates) drops the old records, so a label call on the new workspace
+    without its own baseline fails again."""
+    from deeppicarditeration_amd.data import new_workspace
+    gen = _make("cha", 256, 2)
+    tx, pb = gen.sample_t_and_x(3, point_base=0)
+    odd = 11 * 4096 + 512
+    ws = torch.empty(gen.workspace_bytes(3, 256) + odd, dtype=torch.uint8, device="cuda:0")[odd:]
+    gen.point_baseline(tx, ws=ws)
+    y, _ = gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, ws)
+    torch.cuda.synchronize()
+    L.check(L.load().dpi_workspace_forget(L.c_void_p(ws.data_ptr()), ws.numel()), "dpi_workspace_forget")
+    with pytest.raises(L.DPIError, match="baseline"):
+        gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, ws)
+    fresh = new_workspace(gen.workspace_bytes(3, 256), "cuda:0")
+    with pytest.raises(L.DPIError, match="baseline"):
+        gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, fresh)
+    gen.point_baseline(tx, ws=fresh)
+    assert torch.equal(gen.label_moments_finalize(tx, pb, 256, L.DPI_BOTH, fresh)[0], y)
