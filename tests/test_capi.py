@@ -129,3 +129,15 @@ def test_load_refuses_a_library_built_from_other_sources(monkeypatch):
     # an explicit DPI_HIP_LIB (an A/B variant) is the caller's choice: not checked
     monkeypatch.setenv("DPI_HIP_LIB", str(B.OUT))
     _lib.check_build_id(lib, B.OUT)
+
+
+def test_workspace_forget_is_host_only():
+    """dpi_workspace_forget drops host-side records only (no device work): callable without a GPU on
+    any range, including one that holds no record, and on an empty one."""
+    import ctypes
+
+    from deeppicarditeration_amd import _lib
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(4096)
+    assert lib.dpi_workspace_forget(ctypes.cast(buf, ctypes.c_void_p), 4096) == 0
+    assert lib.dpi_workspace_forget(None, 0) == 0
