@@ -2,7 +2,7 @@
 # One GPU call of a round, by stages: GPU tests, bench lines for every workload, kernel traces (one
 # stream for HJB), the counter list, the VALU / HBM PMC passes, same-box A/B against the round-5
 # package (ab, probe: tools/variants/r05pkg), the N = 2 gloo rehearsals and the RCCL smoke.
-# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|wide|gbmlong|hessab|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
+# usage: tools/gpu_round.sh <tag> [tests|fused|fbab|bench|wide|gbmlong|hessab|hjbfrac|trace|traceb|hjb|hjbprep|counters|pmc|ab|probe|rehearsal|nccl ...]
 #        outputs under gpurun_out/<tag>/
 set -e
 tag=${1:-r02}; shift || true
@@ -42,6 +42,12 @@ for w in $what; do
     for r in 1 2; do
       run 300 $out/bench_gbm_hess_prep_$r.log python bench.py --workload gbm_hess --steps 40 --warmup 3 --no-cpu-baseline --no-fp32-pass --prepare
       run 300 $out/bench_gbm_hess_plain_$r.log python bench.py --workload gbm_hess --steps 40 --warmup 3 --no-cpu-baseline --no-fp32-pass
+    done ;;
+  hjbfrac)  # HJB: the prepared share of the rollout (DPI_PIS_PREP_FRAC), interleaved
+    for r in 1 2; do
+      for f in 0.88 0.92 0.96 1.0; do
+        DPI_PIS_PREP_FRAC=$f run 300 $out/bench_hjb_f${f}_$r.log python bench.py --workload hjb --steps 60 --warmup 3 --no-cpu-baseline --no-fp32-pass
+      done
     done ;;
   hjb)
     run 300 $out/bench_hjb.log python bench.py --workload hjb --steps 10 --warmup 2
