@@ -1683,12 +1683,14 @@ static int pis_prep_shared() {
 // Path sets of a prepared chunk the prepare stream rolls out: DPI_PIS_PREP_FRAC (default 0.92) of
 // them; the shared rollout beside k_pis_net runs at about a third of its stand-alone rate, so the
 // rest goes to the prepared call's head at full occupancy (r04f trace: the prepare-stream rollout
-// of the whole chunk, 4.07 ms, outlasted the 3.75 ms chain it hid under).
+// of the whole chunk, 4.07 ms, outlasted the 3.75 ms chain it hid under).  Round 6 sweeps on two
+// boxes (profiles/r06x, r06y; 60 steps, two runs each): f = 0.88 3.738 / 3.752 and 3.798 / 3.806
+// ms/step against 0.92's 3.763 / 3.774 and 3.831 / 3.827 (0.82: 3.797 / 3.810; 0.96, 1.0, 0.76 slower).
 static int pis_prep_sets(int g) {
   static double f = -1.0;
   if (f < 0.0) {
     const char* e = std::getenv("DPI_PIS_PREP_FRAC");
-    f = e ? std::max(0.0, std::min(1.0, std::atof(e))) : 0.92;
+    f = e ? std::max(0.0, std::min(1.0, std::atof(e))) : 0.88;
   }
   return std::max(0, std::min(g, (int)(f * g + 0.5)));
 }

@@ -45,7 +45,7 @@ for w in $what; do
     done ;;
   hjbfrac)  # HJB: the prepared share of the rollout (DPI_PIS_PREP_FRAC), interleaved
     for r in 1 2; do
-      for f in 0.88 0.92 0.96 1.0; do
+      for f in ${HJB_FRACS:-0.88 0.92 0.96 1.0}; do
         DPI_PIS_PREP_FRAC=$f run 300 $out/bench_hjb_f${f}_$r.log python bench.py --workload hjb --steps 60 --warmup 3 --no-cpu-baseline --no-fp32-pass
       done
     done ;;
